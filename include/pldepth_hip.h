@@ -1,0 +1,219 @@
+/* pldepth_hip.h — C ABI of the MI355X-native (gfx950 / CDNA4) PLDepth training hot path.
+ *
+ * libpldepth_hip.so exports exactly the functions below. Conventions:
+ *   - every entry point returns an int status (PLD_OK = 0); pld_last_error() gives the text;
+ *   - all tensors are CALLER-OWNED DEVICE pointers, fp32 unless stated; activations are NHWC,
+ *     filters are Keras HWIO [kh][kw][cin][cout] unless a function names a native layout;
+ *   - `stream` is a hipStream_t (NULL = default stream); every call is stream-ordered and
+ *     asynchronous, performs no allocation (workspaces are caller-provided, sized by the
+ *     matching *_workspace_size call) and no host synchronisation, so a whole training step can
+ *     be captured into one hipGraph (pld_graph_*);
+ *   - no global mutable state: the library is reentrant across streams and devices.
+ *
+ * The reference (praneeth-b/PLDepth) is pure Python on TF2/Keras and has no FFI; each function
+ * below replaces the TF/Keras op(s) named in its comment (reference file:line). INTEGRATION.md
+ * shows the ctypes binding the reference-side Python would add.
+ */
+#ifndef PLDEPTH_HIP_H
+#define PLDEPTH_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { PLD_OK = 0, PLD_ERR_ARG = 1, PLD_ERR_HIP = 2, PLD_ERR_UNSUPPORTED = 3 };
+
+/* activation selectors (Keras 'relu', 'swish', 'sigmoid') */
+enum { PLD_ACT_NONE = 0, PLD_ACT_RELU = 1, PLD_ACT_SWISH = 2, PLD_ACT_SIGMOID = 3 };
+
+/* sampler strategies (pldepth/data/sampling.py) */
+enum {
+  PLD_SAMPLER_PURE = 0,   /* PurelyMaskedRandomSamplingStrategy     sampling.py:106-150, f=0.8 */
+  PLD_SAMPLER_MASKED = 1, /* MaskedRandomSamplingStrategy           sampling.py:153-170, f=1.5 */
+  PLD_SAMPLER_THRESH = 2, /* ThresholdedMaskedRandomSamplingStrategy sampling.py:172-208, f=1.5 */
+  PLD_SAMPLER_INFO = 3    /* InformationScoreBasedSampling          sampling.py:211-242, f=5   */
+};
+
+const char* pld_last_error(void);
+int pld_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Loss: replaces prepare_fully_fledged_loss_input (pldepth/data/depth_utils.py:39-61) +
+ * FullyFledgedMetaBatchListMLELoss.compute_unreduced_loss (pldepth/losses/nll_loss.py:51-62) +
+ * tfr ListMLELoss + Keras SUM_OVER_BATCH_SIZE, i.e. HourglassNegativeLogLikelihood.__call__
+ * (nll_loss.py:32-40) forward AND its gradient.
+ *   pred   [B][HW]            predicted depth map (y_pred [B,H,W,1])
+ *   y_true [B][R][L][2]       col 0 = flat pixel index as float32, col 1 = gt depth
+ *   nll    [B*R]              per-list negative log-likelihood (workspace/output)
+ *   loss   [1]                mean over the B*R lists
+ *   dpred  [B][HW]            d loss / d pred; zeroed first when zero_dpred != 0, else added to
+ * L may be 1..512. Ties keep a deterministic order (oracle/listmle.py).
+ * ------------------------------------------------------------------------------------------ */
+int pld_listmle_fwd_bwd(const float* pred, const float* y_true, int B, int HW, int R, int L,
+                        float* nll, float* loss, float* dpred, int zero_dpred, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimizer: replaces keras.optimizers.Adam(lr, amsgrad=True) (pldepth/PLDepth.py:133), i.e. TF
+ * ResourceApplyAdamWithAmsgrad on every trainable variable, fused over one flat buffer:
+ *   alpha = lr*sqrt(1-b2^t)/(1-b1^t); g' = grad*grad_scale; m += (g'-m)(1-b1);
+ *   v += (g'^2-v)(1-b2); vhat = max(vhat, v); p -= alpha*m/(sqrt(vhat)+eps)
+ * grad_scale lets a data-parallel caller fold the 1/world averaging into the update.
+ * ------------------------------------------------------------------------------------------ */
+int pld_adam_amsgrad(float* param, const float* grad, float* m, float* v, float* vhat, int64_t n,
+                     float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,
+                     void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Convolution (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32): replaces Keras Conv2D /
+ * TF Conv2D + Conv2DBackpropInput + Conv2DBackpropFilter (pl_hourglass.py:59-96 decoder, the
+ * EfficientNetB0 1x1/3x3 convs, redweb.py convs). The input may be the channel concatenation of
+ * two NHWC tensors (layers.Concatenate, pl_hourglass.py:66,75,84) — no concat is materialised.
+ * Padding is explicit (TF 'same' = pad_t = ((oh-1)*sh + kh - h)/2 rounded down, rest at the
+ * bottom; ZeroPadding2D(correct_pad) likewise).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct pld_conv_args {
+  const float* x1;  /* [n][h][w][c1] */
+  const float* x2;  /* [n][h][w][c2] or NULL (c2 = 0) */
+  int c1, c2;
+  int n, h, w;
+  int kh, kw, sh, sw, pad_t, pad_l;
+  int oh, ow;
+  int cout;
+  /* optional input prologue applied to in-bounds pixels of x1 (fuses BN-apply + act of the
+   * producer): x' = act(x*in_scale[c] + in_shift[c]); NULL scale = identity */
+  const float* in_scale;
+  const float* in_shift;
+  int in_act;
+} pld_conv_args;
+
+/* forward: y[n][oh][ow][cout] (+)= conv(x, W) + bias.  w_ohwi = native layout
+ * [cout][kh][kw][c1+c2] (pld_filter_to_native).  bias may be NULL. */
+int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias, float* y,
+                   int accumulate, void* stream);
+
+/* input gradient for stride-1 convolutions: dx = conv^T(dy, W).  w_dgrad = native layout
+ * [c1+c2][kh][kw][cout] with the taps flipped (pld_filter_to_dgrad).  dx1 receives channels
+ * [0,c1), dx2 channels [c1,c1+c2); each is overwritten or accumulated per its flag. */
+int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad, float* dx1,
+                     int accumulate1, float* dx2, int accumulate2, void* stream);
+
+/* filter gradient: dw[kh][kw][c1+c2][cout] (HWIO) (+)= sum over pixels of x (x) dy.
+ * Deterministic split-K: partial slabs in `ws`, then an ordered reduction. */
+size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a);
+int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* dw, int accumulate, void* ws,
+                     size_t ws_bytes, void* stream);
+
+/* HWIO [kh][kw][cin][cout] -> forward native [cout][kh][kw][cin] */
+int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_ohwi,
+                         void* stream);
+/* HWIO -> dgrad native [cin][kh][kw][cout] with flipped taps (kh-1-i, kw-1-j) */
+int pld_filter_to_dgrad(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_dgrad,
+                        void* stream);
+
+/* per-channel column sum over `rows` rows of an [rows][c] tensor: out[c] (+)= sum_r x[r][c]
+ * (bias gradient of Conv2D). ws >= pld_channel_reduce_workspace_size(rows, c). */
+size_t pld_channel_reduce_workspace_size(int64_t rows, int c);
+int pld_channel_sum(const float* x, int64_t rows, int c, float* out, int accumulate, void* ws,
+                    void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * BatchNormalization in training mode (Keras BatchNormalization, TF FusedBatchNormV3 + grad):
+ * every BN of pl_hourglass.py:60-92, the 49 EfficientNet BNs (trainable, :52-57), redweb.py BNs.
+ * Batch statistics over all rows of an NHWC tensor viewed as [rows][c]; biased variance for the
+ * normalisation, unbiased for the moving-variance update (momentum as Keras: new = old*mom +
+ * batch*(1-mom)). Statistics accumulate in fp64.
+ * ------------------------------------------------------------------------------------------ */
+int pld_bn_stats(const float* x, int64_t rows, int c, float eps, float momentum, float* mean,
+                 float* invstd, float* moving_mean, float* moving_var, void* ws, void* stream);
+/* y = act(((x-mean)*invstd)*gamma + beta) [* gate[img][c]]  (gate = SE excitation, may be NULL;
+ * hw = rows per image, used only with gate) */
+int pld_bn_apply(const float* x, int64_t rows, int c, const float* mean, const float* invstd,
+                 const float* gamma, const float* beta, int act, const float* gate, int hw,
+                 float* y, void* stream);
+/* backward of y = act(bn(x)):  dy_eff = dy*(gate?gate[img][c]:1) + (addn?addn[img][c]:0);
+ * dz = dy_eff*act'(z); dgamma (+)= sum dz*xhat; dbeta (+)= sum dz;
+ * dx (=|+=) invstd*gamma*(dz - mean(dz) - xhat*mean(dz*xhat)). */
+int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+               const float* invstd, const float* gamma, const float* beta, int act,
+               const float* gate, const float* addn, int hw, float* dx, int dx_accumulate,
+               float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Elementwise / resampling
+ * ------------------------------------------------------------------------------------------ */
+/* y = act(x*scale[c] + shift[c]) (input normalisation, bias+act) over [rows][c] */
+int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
+                           const float* shift, int act, float* y, void* stream);
+/* UpSampling2D(interpolation='bilinear') x2, half-pixel centres (pl_hourglass.py:62..94):
+ * x [n][h][w][c] -> y [n][2h][2w][c];  bwd: dx [n][h][w][c] (=|+=) adjoint(dy) */
+int pld_upsample2x_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream);
+int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx, int accumulate,
+                       void* stream);
+/* y = a * sample_scale[img] + b  (EfficientNet drop-connect Dropout(noise_shape=(N,1,1,1)) +
+ * residual add); sample_scale may be NULL (=1). rows_per_img*c elements per image. */
+int pld_residual_add(const float* a, const float* sample_scale, const float* b, int n,
+                     int64_t elems_per_img, float* y, void* stream);
+/* y[i] = x[i] * sample_scale[img] (+ y[i] when accumulate) */
+int pld_scale_per_sample(const float* x, const float* sample_scale, int n, int64_t elems_per_img,
+                         float* y, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * EfficientNet depthwise conv (DepthwiseConv2D, no bias) fwd and input gradient; filter
+ * [k][k][c]; any stride, explicit (possibly asymmetric) padding.
+ * ------------------------------------------------------------------------------------------ */
+int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const float* wdw, int k, int s,
+                   int pad_t, int pad_l, int oh, int ow, float* y, void* stream);
+int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw, int k, int s,
+                     int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
+                     void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * EfficientNet squeeze-and-excitation (frozen FCs, gradient flows to the input):
+ *   pooled = mean_hw(a); z1 = pooled@w1 + b1; h1 = swish(z1); z2 = h1@w2 + b2; gate = sigmoid(z2)
+ * (the caller applies a*gate, e.g. via pld_bn_apply's gate). w1 [c][cse], w2 [cse][c].
+ * pld_se_bwd: given dy (grad of a*gate) and a, produces gate (unchanged) and addn[n][c] =
+ * d(pooled)/hw so that da = dy*gate + addn (consumed by pld_bn_bwd's gate/addn).
+ * ------------------------------------------------------------------------------------------ */
+size_t pld_se_workspace_size(int n, int hw, int c, int cse);
+int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const float* w1, const float* b1,
+               const float* w2, const float* b2, float* pooled, float* z1, float* gate, void* ws,
+               void* stream);
+int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c, int cse, const float* w1,
+               const float* w2, const float* z1, const float* gate, float* addn, void* ws,
+               void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Ranking sampler (pldepth/data/sampling.py), split into draws and a deterministic part.
+ *   pld_sampler_compact: mask [B][H][W] (>0 valid) -> valid_idx [B][H*W] (row-major flat
+ *       positions, np.where order), nvalid [B]; also gt min/max per image (Info strategy).
+ *   pld_sampler_draw: Philox4x32-10 draws[b][cand][slot] in [0, nvalid[b]) keyed by
+ *       (seed, step, image_offset + b, cand*L + slot) — independent of the GPU count.
+ *   pld_sampler_rank: gather + per-list descending sort + strategy score + top-R selection,
+ *       bit-identical to oracle/sampler.py for the same draws. out [B][R_out][L][2] float32
+ *       (R_out = R, or floor(0.8R) for PURE).
+ * ------------------------------------------------------------------------------------------ */
+size_t pld_sampler_workspace_size(int B, int H, int W, int R, int L, int strategy);
+int pld_sampler_compact(const float* mask, int B, int H, int W, const float* gt, int* valid_idx,
+                        int* nvalid, float* gt_minmax, void* ws, void* stream);
+int pld_sampler_draw(const int* nvalid, int B, int n_cand, int L, uint64_t seed, uint64_t step,
+                     int image_offset, int* draws, void* stream);
+int pld_sampler_rank(const float* gt, const int* valid_idx, const int* nvalid,
+                     const float* gt_minmax, const int* draws, int B, int H, int W, int R, int L,
+                     int strategy, float* out, void* ws, void* stream);
+int pld_sampler_candidates(int R, int strategy); /* int(R * factor) */
+
+/* ------------------------------------------------------------------------------------------
+ * hipGraph capture of a whole stream-ordered step (replaces Keras' per-op dispatch)
+ * ------------------------------------------------------------------------------------------ */
+int pld_graph_begin(void* stream);
+int pld_graph_end(void* stream, void** graph_exec);
+int pld_graph_launch(void* graph_exec, void* stream);
+int pld_graph_destroy(void* graph_exec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLDEPTH_HIP_H */

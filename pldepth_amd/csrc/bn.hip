@@ -1,0 +1,497 @@
+// Training-mode BatchNormalization (+ fused activation / SE gate) and per-channel reductions.
+//
+// Replaces Keras BatchNormalization in training mode (TF FusedBatchNormV3 / FusedBatchNormGradV3)
+// for every BN on the hot path: the decoder BNs (pldepth/models/pl_hourglass.py:60,69,78,87,92),
+// the 49 trainable EfficientNetB0 BNs (frozen encoder, BN trainable: pl_hourglass.py:52-57) and
+// the ReDWeb/ResNet BNs (redweb.py). Keras defaults: epsilon 1e-3, momentum 0.99; the moving
+// variance is updated with the unbiased (n/(n-1)) batch variance, the output uses the biased one.
+//
+// Channel reductions run over an NHWC tensor viewed as [rows][C]: a block owns a row range and up
+// to 256 float4 channel groups; each thread accumulates in fp64 (the statistics of 6.4M-row
+// tensors stay exact to ~1e-16), block partials land in a caller workspace and a finalize kernel
+// sums them in a fixed order (deterministic, no atomics). HBM-bound: one read of x (stats) and
+// one read of (x, dy) (backward) per element.
+#include <algorithm>
+
+#include "common.h"
+
+namespace pld {
+
+enum RedOp { RED_STATS = 0, RED_SUM = 1, RED_BNBWD = 2 };
+
+struct RedParams {
+  const float* x;
+  const float* dy;
+  long rows;
+  int C;
+  int rows_per_block;
+  // BNBWD
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  const float* gate;
+  const float* addn;
+  FastDiv dHW;
+  double* partial;  // [gridDim.x][C][2]
+};
+
+template <int VW>
+__device__ __forceinline__ void ld(const float* p, float (&v)[VW]) {
+  if constexpr (VW == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int OP, int VW>
+__global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
+  __shared__ double red[256][2 * VW];
+  const int CV = p.C / VW;
+  const int cbase = blockIdx.y * 256;
+  const int ncv = min(256, CV - cbase);
+  const int tid = threadIdx.x;
+  const int rpi = 256 / ncv;
+  const int r0 = tid / ncv;
+  const int cv = cbase + tid % ncv;
+  const bool act = r0 < rpi;
+  const long rbeg = (long)blockIdx.x * p.rows_per_block;
+  const long rend = min(p.rows, rbeg + p.rows_per_block);
+  double s0[VW], s1[VW];
+#pragma unroll
+  for (int u = 0; u < VW; ++u) s0[u] = s1[u] = 0.0;
+  if (act) {
+    const int c0 = cv * VW;
+    float mean[VW], inv[VW], gam[VW], bet[VW];
+    if (OP == RED_BNBWD) {
+      ld<VW>(p.mean + c0, mean);
+      ld<VW>(p.invstd + c0, inv);
+      ld<VW>(p.gamma + c0, gam);
+      ld<VW>(p.beta + c0, bet);
+    }
+    for (long r = rbeg + r0; r < rend; r += rpi) {
+      float xv[VW];
+      ld<VW>(p.x + r * p.C + c0, xv);
+      if (OP == RED_STATS) {
+#pragma unroll
+        for (int u = 0; u < VW; ++u) {
+          const double d = xv[u];
+          s0[u] += d;
+          s1[u] += d * d;
+        }
+      } else if (OP == RED_SUM) {
+#pragma unroll
+        for (int u = 0; u < VW; ++u) s0[u] += (double)xv[u];
+      } else {
+        float dv[VW];
+        ld<VW>(p.dy + r * p.C + c0, dv);
+        float g[VW], a[VW];
+        const long img = (p.gate || p.addn) ? (long)p.dHW.div((uint32_t)r) : 0;
+#pragma unroll
+        for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
+        if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
+        if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) {
+          const float xh = (xv[u] - mean[u]) * inv[u];
+          const float z = xh * gam[u] + bet[u];
+          const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
+          s0[u] += (double)dz;
+          s1[u] += (double)dz * (double)xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < VW; ++u) {
+    red[tid][u] = s0[u];
+    red[tid][VW + u] = s1[u];
+  }
+  __syncthreads();
+  if (act && r0 == 0) {
+    for (int j = 1; j < rpi; ++j) {
+#pragma unroll
+      for (int u = 0; u < VW; ++u) {
+        s0[u] += red[tid + j * ncv][u];
+        s1[u] += red[tid + j * ncv][VW + u];
+      }
+    }
+    double* out = p.partial + ((long)blockIdx.x * p.C + cv * VW) * 2;
+#pragma unroll
+    for (int u = 0; u < VW; ++u) {
+      out[2 * u] = s0[u];
+      out[2 * u + 1] = s1[u];
+    }
+  }
+}
+
+static void red_plan(long rows, int C, int& nbx, int& rpb) {
+  // ~ 2048 blocks total, >= 32 rows per block
+  const int cy = (int)cdiv(C / ((C % 4 == 0) ? 4 : 1), 256);
+  long want = std::max<long>(1, 2048 / cy);
+  rpb = (int)std::max<long>(32, (rows + want - 1) / want);
+  nbx = (int)((rows + rpb - 1) / rpb);
+}
+
+static int launch_reduce(int op, RedParams& p, hipStream_t st) {
+  int nbx, rpb;
+  red_plan(p.rows, p.C, nbx, rpb);
+  p.rows_per_block = rpb;
+  const bool v4 = (p.C % 4 == 0);
+  const int CV = p.C / (v4 ? 4 : 1);
+  dim3 grid(nbx, cdiv(CV, 256));
+#define PLD_RED(OPV)                                                                         \
+  if (v4) chan_reduce_kernel<OPV, 4><<<grid, 256, 0, st>>>(p);                               \
+  else chan_reduce_kernel<OPV, 1><<<grid, 256, 0, st>>>(p);
+  if (op == RED_STATS) { PLD_RED(RED_STATS) }
+  else if (op == RED_SUM) { PLD_RED(RED_SUM) }
+  else { PLD_RED(RED_BNBWD) }
+#undef PLD_RED
+  return check_launch("chan_reduce_kernel");
+}
+
+// ---- finalize kernels: sum the nbx partials of each channel in order ----
+__global__ void stats_finalize_kernel(const double* __restrict__ part, int nbx, int C, long rows,
+                                      float eps, float momentum, float* __restrict__ mean,
+                                      float* __restrict__ invstd, float* __restrict__ mmean,
+                                      float* __restrict__ mvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nbx; ++b) {
+    s += part[((long)b * C + c) * 2];
+    q += part[((long)b * C + c) * 2 + 1];
+  }
+  const double n = (double)rows;
+  const double mu = s / n;
+  double var = q / n - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (mmean) {
+    const double uvar = rows > 1 ? var * n / (n - 1.0) : var;
+    // Keras assign_moving_average: v -= (v - value) * (1 - momentum)
+    mmean[c] = mmean[c] - (mmean[c] - (float)mu) * (1.0f - momentum);
+    mvar[c] = mvar[c] - (mvar[c] - (float)uvar) * (1.0f - momentum);
+  }
+}
+
+__global__ void sum_finalize_kernel(const double* __restrict__ part, int nbx, int C,
+                                    float* __restrict__ out, int acc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < nbx; ++b) s += part[((long)b * C + c) * 2];
+  out[c] = acc ? out[c] + (float)s : (float)s;
+}
+
+// writes dgamma/dbeta and the per-channel coefficients k1 = mean(dz), k2 = mean(dz*xhat)
+__global__ void bnbwd_finalize_kernel(const double* __restrict__ part, int nbx, int C, long rows,
+                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                      int pacc, float* __restrict__ k12) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nbx; ++b) {
+    s += part[((long)b * C + c) * 2];
+    q += part[((long)b * C + c) * 2 + 1];
+  }
+  if (dbeta) dbeta[c] = pacc ? dbeta[c] + (float)s : (float)s;
+  if (dgamma) dgamma[c] = pacc ? dgamma[c] + (float)q : (float)q;
+  k12[c] = (float)(s / (double)rows);
+  k12[C + c] = (float)(q / (double)rows);
+}
+
+// ---- elementwise ----
+struct ApplyParams {
+  const float* x;
+  long rows;
+  int C;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  const float* scale;  // affine form (mean == NULL): y = act(x*scale + shift)
+  const float* shift;
+  int act;
+  const float* gate;
+  FastDiv dHW;
+  FastDiv dCV;
+  float* y;
+};
+
+template <int VW>
+__global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
+  const long nv = p.rows * p.C / VW;
+  const int CV = p.C / VW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nv;
+       e += (long)gridDim.x * blockDim.x) {
+    const long r = (long)p.dCV.div((uint32_t)e);
+    const int c0 = (int)(e - r * CV) * VW;
+    float xv[VW], a[VW], b[VW], g[VW];
+    ld<VW>(p.x + e * VW, xv);
+    if (p.mean) {
+      float mu[VW], is[VW], ga[VW], be[VW];
+      ld<VW>(p.mean + c0, mu);
+      ld<VW>(p.invstd + c0, is);
+      ld<VW>(p.gamma + c0, ga);
+      ld<VW>(p.beta + c0, be);
+#pragma unroll
+      for (int u = 0; u < VW; ++u) {
+        a[u] = xv[u] - mu[u];
+        b[u] = is[u];
+        xv[u] = (a[u] * b[u]) * ga[u] + be[u];
+      }
+    } else {
+      ld<VW>(p.scale + c0, a);
+      ld<VW>(p.shift + c0, b);
+#pragma unroll
+      for (int u = 0; u < VW; ++u) xv[u] = xv[u] * a[u] + b[u];
+    }
+#pragma unroll
+    for (int u = 0; u < VW; ++u) g[u] = 1.f;
+    if (p.gate) ld<VW>(p.gate + (long)p.dHW.div((uint32_t)r) * p.C + c0, g);
+#pragma unroll
+    for (int u = 0; u < VW; ++u) xv[u] = act_fwd(p.act, xv[u]) * g[u];
+    if constexpr (VW == 4)
+      *reinterpret_cast<float4*>(p.y + e * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+    else
+      p.y[e] = xv[0];
+  }
+}
+
+struct BwdApplyParams {
+  const float* x;
+  const float* dy;
+  long rows;
+  int C;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  const float* gate;
+  const float* addn;
+  FastDiv dHW;
+  const float* k12;
+  float* dx;
+  int acc;
+  FastDiv dCV;
+};
+
+template <int VW>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
+  const long nv = p.rows * p.C / VW;
+  const int CV = p.C / VW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nv;
+       e += (long)gridDim.x * blockDim.x) {
+    const long r = (long)p.dCV.div((uint32_t)e);
+    const int c0 = (int)(e - r * CV) * VW;
+    float xv[VW], dv[VW], mu[VW], is[VW], ga[VW], be[VW], k1[VW], k2[VW], g[VW], a[VW];
+    ld<VW>(p.x + e * VW, xv);
+    ld<VW>(p.dy + e * VW, dv);
+    ld<VW>(p.mean + c0, mu);
+    ld<VW>(p.invstd + c0, is);
+    ld<VW>(p.gamma + c0, ga);
+    ld<VW>(p.beta + c0, be);
+    ld<VW>(p.k12 + c0, k1);
+    ld<VW>(p.k12 + p.C + c0, k2);
+#pragma unroll
+    for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
+    if (p.gate || p.addn) {
+      const long img = (long)p.dHW.div((uint32_t)r);
+      if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
+      if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
+    }
+    float o[VW];
+#pragma unroll
+    for (int u = 0; u < VW; ++u) {
+      const float xh = (xv[u] - mu[u]) * is[u];
+      const float z = xh * ga[u] + be[u];
+      const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
+      o[u] = (is[u] * ga[u]) * (dz - k1[u] - xh * k2[u]);
+    }
+    if constexpr (VW == 4) {
+      float4* d = reinterpret_cast<float4*>(p.dx + e * 4);
+      float4 v = make_float4(o[0], o[1], o[2], o[3]);
+      if (p.acc) {
+        const float4 old = *d;
+        v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+      }
+      *d = v;
+    } else {
+      p.dx[e] = p.acc ? p.dx[e] + o[0] : o[0];
+    }
+  }
+}
+
+static unsigned ew_grid(long nv) { return std::min<unsigned>(std::max(cdiv(nv, 256), 1u), 8192); }
+
+static size_t red_ws_doubles(long rows, int C) {
+  int nbx, rpb;
+  red_plan(rows, C, nbx, rpb);
+  return (size_t)nbx * C * 2;
+}
+
+}  // namespace pld
+
+using namespace pld;
+
+extern "C" size_t pld_channel_reduce_workspace_size(int64_t rows, int c) {
+  if (rows <= 0 || c <= 0) return 0;
+  // fp64 partials + 2*C floats of BN-backward coefficients
+  return red_ws_doubles(rows, c) * sizeof(double) + 2 * sizeof(float) * (size_t)c + 64;
+}
+
+extern "C" int pld_channel_sum(const float* x, int64_t rows, int c, float* out, int accumulate,
+                               void* ws, void* stream) {
+  PLD_CHECK_ARG(x && out && ws && rows > 0 && c > 0, "pld_channel_sum: bad args");
+  PLD_CHECK_ARG(rows < (1L << 31), "pld_channel_sum: too many rows");
+  RedParams p{};
+  p.x = x;
+  p.rows = rows;
+  p.C = c;
+  p.partial = (double*)ws;
+  hipStream_t st = as_stream(stream);
+  int rc = launch_reduce(RED_SUM, p, st);
+  if (rc) return rc;
+  int nbx, rpb;
+  red_plan(rows, c, nbx, rpb);
+  sum_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, out, accumulate);
+  return check_launch("sum_finalize_kernel");
+}
+
+extern "C" int pld_bn_stats(const float* x, int64_t rows, int c, float eps, float momentum,
+                            float* mean, float* invstd, float* moving_mean, float* moving_var,
+                            void* ws, void* stream) {
+  PLD_CHECK_ARG(x && mean && invstd && ws && rows > 0 && c > 0, "pld_bn_stats: bad args");
+  PLD_CHECK_ARG(rows < (1L << 31), "pld_bn_stats: too many rows");
+  PLD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr),
+                "pld_bn_stats: moving_mean/moving_var must both be given or both NULL");
+  RedParams p{};
+  p.x = x;
+  p.rows = rows;
+  p.C = c;
+  p.partial = (double*)ws;
+  hipStream_t st = as_stream(stream);
+  int rc = launch_reduce(RED_STATS, p, st);
+  if (rc) return rc;
+  int nbx, rpb;
+  red_plan(rows, c, nbx, rpb);
+  stats_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, rows, eps, momentum,
+                                                       mean, invstd, moving_mean, moving_var);
+  return check_launch("stats_finalize_kernel");
+}
+
+extern "C" int pld_bn_apply(const float* x, int64_t rows, int c, const float* mean,
+                            const float* invstd, const float* gamma, const float* beta, int act,
+                            const float* gate, int hw, float* y, void* stream) {
+  PLD_CHECK_ARG(x && y && mean && invstd && gamma && beta && rows > 0 && c > 0,
+                "pld_bn_apply: bad args");
+  PLD_CHECK_ARG(!gate || hw > 0, "pld_bn_apply: gate needs hw > 0");
+  ApplyParams p{};
+  p.x = x;
+  p.rows = rows;
+  p.C = c;
+  p.mean = mean;
+  p.invstd = invstd;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.act = act;
+  p.gate = gate;
+  p.dHW = FastDiv((uint32_t)std::max(hw, 1));
+  p.y = y;
+  p.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
+  PLD_CHECK_ARG(rows * c < (1L << 31), "elementwise: tensor too large");
+  hipStream_t st = as_stream(stream);
+  if (c % 4 == 0) {
+    bn_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(p);
+  } else {
+    bn_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(p);
+  }
+  return check_launch("bn_apply_kernel");
+}
+
+extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
+                                      const float* shift, int act, float* y, void* stream) {
+  PLD_CHECK_ARG(x && y && scale && shift && rows > 0 && c > 0, "pld_channel_affine_act: bad args");
+  ApplyParams p{};
+  p.x = x;
+  p.rows = rows;
+  p.C = c;
+  p.scale = scale;
+  p.shift = shift;
+  p.act = act;
+  p.dHW = FastDiv(1);
+  p.y = y;
+  p.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
+  PLD_CHECK_ARG(rows * c < (1L << 31), "elementwise: tensor too large");
+  hipStream_t st = as_stream(stream);
+  if (c % 4 == 0) {
+    bn_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(p);
+  } else {
+    bn_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(p);
+  }
+  return check_launch("bn_apply_kernel(affine)");
+}
+
+extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, int act,
+                          const float* gate, const float* addn, int hw, float* dx,
+                          int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate,
+                          void* ws, void* stream) {
+  PLD_CHECK_ARG(x && dy && mean && invstd && gamma && beta && ws && rows > 0 && c > 0,
+                "pld_bn_bwd: bad args");
+  PLD_CHECK_ARG(rows < (1L << 31), "pld_bn_bwd: too many rows");
+  PLD_CHECK_ARG(!(gate || addn) || hw > 0, "pld_bn_bwd: gate/addn need hw > 0");
+  hipStream_t st = as_stream(stream);
+  RedParams p{};
+  p.x = x;
+  p.dy = dy;
+  p.rows = rows;
+  p.C = c;
+  p.mean = mean;
+  p.invstd = invstd;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.act = act;
+  p.gate = gate;
+  p.addn = addn;
+  p.dHW = FastDiv((uint32_t)std::max(hw, 1));
+  p.partial = (double*)ws;
+  int rc = launch_reduce(RED_BNBWD, p, st);
+  if (rc) return rc;
+  int nbx, rpb;
+  red_plan(rows, c, nbx, rpb);
+  float* k12 = reinterpret_cast<float*>((char*)ws + red_ws_doubles(rows, c) * sizeof(double));
+  bnbwd_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
+                                                       param_accumulate, k12);
+  rc = check_launch("bnbwd_finalize_kernel");
+  if (rc || !dx) return rc;
+  BwdApplyParams q{};
+  q.x = x;
+  q.dy = dy;
+  q.rows = rows;
+  q.C = c;
+  q.mean = mean;
+  q.invstd = invstd;
+  q.gamma = gamma;
+  q.beta = beta;
+  q.act = act;
+  q.gate = gate;
+  q.addn = addn;
+  q.dHW = p.dHW;
+  q.k12 = k12;
+  q.dx = dx;
+  q.acc = dx_accumulate;
+  q.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
+  if (c % 4 == 0) {
+    bn_bwd_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(q);
+  } else {
+    bn_bwd_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(q);
+  }
+  return check_launch("bn_bwd_apply_kernel");
+}

@@ -1,0 +1,199 @@
+// Bilinear x2 upsampling (fwd + adjoint) and the per-sample residual combine.
+//
+// UpSampling2D(interpolation='bilinear') (pldepth/models/pl_hourglass.py:62,71,80,89,94) resolves
+// to tf.image.resize(bilinear, half_pixel_centers=True): out row o samples in = (o+0.5)/2-0.5,
+// lower = max(floor(in),0), upper = min(ceil(in), h-1), lerp = in-floor(in); computed here in the
+// same lerp form (top + (bottom-top)*ylerp). The gradient (ResizeBilinearGrad) is the adjoint,
+// written as a gather: input row k receives output rows 2k-1 (w .25), 2k (w .75, or 1 at k=0),
+// 2k+1 (w .75, or 1 at k=h-1), 2k+2 (w .25); the 2-D weight is the product of the 1-D weights.
+// Both are HBM-bound, float4 over channels.
+//
+// pld_residual_add: EfficientNet block output = Dropout(noise_shape=(N,1,1,1))(x) + inputs
+// (keras efficientnet.py block(), drop-connect rate 0.2*b/16): a per-sample keep/(1-rate) scale.
+#include <algorithm>
+
+#include "common.h"
+
+namespace pld {
+
+template <int VW>
+__device__ __forceinline__ void ld4(const float* p, float (&v)[VW]) {
+  if constexpr (VW == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int VW>
+__device__ __forceinline__ void st4(float* p, const float (&v)[VW]) {
+  if constexpr (VW == 4)
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    *p = v[0];
+}
+
+__device__ __forceinline__ void lerp_coords(int o, int in_size, int& lo, int& hi, float& l) {
+  const float in = ((float)o + 0.5f) * 0.5f - 0.5f;
+  const float f = floorf(in);
+  lo = max((int)f, 0);
+  hi = min((int)ceilf(in), in_size - 1);
+  l = in - f;
+}
+
+template <int VW>
+__global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __restrict__ x, int n,
+                                                             int h, int w, int c,
+                                                             float* __restrict__ y) {
+  const int cv = c / VW;
+  const int H2 = 2 * h, W2 = 2 * w;
+  const long total = (long)n * H2 * W2 * cv;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(e % cv);
+    long t = e / cv;
+    const int ox = (int)(t % W2);
+    t /= W2;
+    const int oy = (int)(t % H2);
+    const int img = (int)(t / H2);
+    int y0, y1, x0, x1;
+    float yl, xl;
+    lerp_coords(oy, h, y0, y1, yl);
+    lerp_coords(ox, w, x0, x1, xl);
+    const float* base = x + (long)img * h * w * c + q * VW;
+    float tl[VW], tr[VW], bl[VW], br[VW], o[VW];
+    ld4<VW>(base + ((long)y0 * w + x0) * c, tl);
+    ld4<VW>(base + ((long)y0 * w + x1) * c, tr);
+    ld4<VW>(base + ((long)y1 * w + x0) * c, bl);
+    ld4<VW>(base + ((long)y1 * w + x1) * c, br);
+#pragma unroll
+    for (int u = 0; u < VW; ++u) {
+      const float top = tl[u] + (tr[u] - tl[u]) * xl;
+      const float bot = bl[u] + (br[u] - bl[u]) * xl;
+      o[u] = top + (bot - top) * yl;
+    }
+    st4<VW>(y + e * VW, o);
+  }
+}
+
+// 1-D adjoint taps of input index k (size s): output indices and weights
+__device__ __forceinline__ int adj_taps(int k, int s, int (&o)[4], float (&wt)[4]) {
+  int cnt = 0;
+  if (k >= 1) { o[cnt] = 2 * k - 1; wt[cnt++] = 0.25f; }
+  o[cnt] = 2 * k; wt[cnt++] = (k == 0) ? 1.0f : 0.75f;
+  o[cnt] = 2 * k + 1; wt[cnt++] = (k == s - 1) ? 1.0f : 0.75f;
+  if (k <= s - 2) { o[cnt] = 2 * k + 2; wt[cnt++] = 0.25f; }
+  return cnt;
+}
+
+template <int VW>
+__global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const float* __restrict__ dy, int n,
+                                                             int h, int w, int c,
+                                                             float* __restrict__ dx, int acc) {
+  const int cv = c / VW;
+  const int W2 = 2 * w;
+  const long total = (long)n * h * w * cv;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(e % cv);
+    long t = e / cv;
+    const int kx = (int)(t % w);
+    t /= w;
+    const int ky = (int)(t % h);
+    const int img = (int)(t / h);
+    int oy[4], ox[4];
+    float wy[4], wx[4];
+    const int ny = adj_taps(ky, h, oy, wy);
+    const int nx = adj_taps(kx, w, ox, wx);
+    const float* base = dy + (long)img * 2 * h * W2 * c + q * VW;
+    float s[VW];
+#pragma unroll
+    for (int u = 0; u < VW; ++u) s[u] = 0.f;
+    for (int a = 0; a < ny; ++a) {
+      float rs[VW];
+#pragma unroll
+      for (int u = 0; u < VW; ++u) rs[u] = 0.f;
+      for (int b = 0; b < nx; ++b) {
+        float v[VW];
+        ld4<VW>(base + ((long)oy[a] * W2 + ox[b]) * c, v);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) rs[u] += wx[b] * v[u];
+      }
+#pragma unroll
+      for (int u = 0; u < VW; ++u) s[u] += wy[a] * rs[u];
+    }
+    if (acc) {
+      float old[VW];
+      ld4<VW>(dx + e * VW, old);
+#pragma unroll
+      for (int u = 0; u < VW; ++u) s[u] += old[u];
+    }
+    st4<VW>(dx + e * VW, s);
+  }
+}
+
+__global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__ a,
+                                                       const float* __restrict__ sc,
+                                                       const float* __restrict__ b, long per,
+                                                       long total, float* __restrict__ y,
+                                                       int acc) {
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const float s = sc ? sc[e / per] : 1.f;
+    float v = a[e] * s;
+    if (b) v += b[e];
+    if (acc) v += y[e];
+    y[e] = v;
+  }
+}
+
+static unsigned grid_for(long n) { return std::min<unsigned>(std::max(cdiv(n, 256), 1u), 8192); }
+
+}  // namespace pld
+
+using namespace pld;
+
+extern "C" int pld_upsample2x_fwd(const float* x, int n, int h, int w, int c, float* y,
+                                  void* stream) {
+  PLD_CHECK_ARG(x && y && n > 0 && h > 0 && w > 0 && c > 0, "pld_upsample2x_fwd: bad args");
+  hipStream_t st = as_stream(stream);
+  const long total = (long)n * 4 * h * w * c;
+  if (c % 4 == 0)
+    upsample2x_fwd_kernel<4><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, y);
+  else
+    upsample2x_fwd_kernel<1><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, y);
+  return check_launch("upsample2x_fwd_kernel");
+}
+
+extern "C" int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx,
+                                  int accumulate, void* stream) {
+  PLD_CHECK_ARG(dy && dx && n > 0 && h > 0 && w > 0 && c > 0, "pld_upsample2x_bwd: bad args");
+  hipStream_t st = as_stream(stream);
+  const long total = (long)n * h * w * c;
+  if (c % 4 == 0)
+    upsample2x_bwd_kernel<4><<<grid_for(total / 4), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate);
+  else
+    upsample2x_bwd_kernel<1><<<grid_for(total), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate);
+  return check_launch("upsample2x_bwd_kernel");
+}
+
+extern "C" int pld_residual_add(const float* a, const float* sample_scale, const float* b, int n,
+                                int64_t elems_per_img, float* y, void* stream) {
+  PLD_CHECK_ARG(a && y && n > 0 && elems_per_img > 0, "pld_residual_add: bad args");
+  const long total = (long)n * elems_per_img;
+  residual_kernel<<<grid_for(total), 256, 0, as_stream(stream)>>>(a, sample_scale, b,
+                                                                  elems_per_img, total, y, 0);
+  return check_launch("residual_kernel");
+}
+
+extern "C" int pld_scale_per_sample(const float* x, const float* sample_scale, int n,
+                                    int64_t elems_per_img, float* y, int accumulate,
+                                    void* stream) {
+  PLD_CHECK_ARG(x && y && n > 0 && elems_per_img > 0, "pld_scale_per_sample: bad args");
+  const long total = (long)n * elems_per_img;
+  residual_kernel<<<grid_for(total), 256, 0, as_stream(stream)>>>(x, sample_scale, nullptr,
+                                                                  elems_per_img, total, y,
+                                                                  accumulate);
+  return check_launch("residual_kernel(scale)");
+}

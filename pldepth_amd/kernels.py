@@ -1,0 +1,234 @@
+"""Thin Python wrappers over the C ABI, taking torch device tensors as memory handles.
+
+PyTorch is plumbing here: tensors provide device memory and the current HIP stream; every
+computation is a call into libpldepth_hip.so. Nothing here falls back to torch math.
+"""
+import ctypes as C
+
+import torch
+
+from ._lib import ConvArgs, lib
+
+ACT = {"none": 0, "linear": 0, None: 0, "relu": 1, "swish": 2, "sigmoid": 3}
+SAMPLER = {"pure": 0, "masked": 1, "thresh": 2, "info": 3}
+
+
+def ptr(t):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "device tensors must be contiguous HIP tensors"
+    return C.c_void_p(t.data_ptr())
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _f32(t):
+    assert t.dtype == torch.float32, t.dtype
+    return t
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, key="default"):
+    """Reusable byte workspace on the current device (grown on demand, never shrunk)."""
+    dev = torch.cuda.current_device()
+    k = (dev, key)
+    buf = _ws_cache.get(k)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device="cuda")
+        _ws_cache[k] = buf
+    return buf
+
+
+# ------------------------------------------------------------------------------------- loss
+def listmle_fwd_bwd(pred, y_true, B, R, L, dpred=None, nll=None, loss=None, zero_dpred=True):
+    HW = pred.numel() // B
+    dpred = torch.empty_like(pred) if dpred is None else dpred
+    nll = torch.empty(B * R, dtype=torch.float32, device=pred.device) if nll is None else nll
+    loss = torch.empty(1, dtype=torch.float32, device=pred.device) if loss is None else loss
+    lib().pld_listmle_fwd_bwd(ptr(_f32(pred)), ptr(_f32(y_true)), B, HW, R, L, ptr(nll),
+                              ptr(loss), ptr(dpred), int(zero_dpred), stream())
+    return loss, dpred, nll
+
+
+# ------------------------------------------------------------------------------- optimizer
+def adam_amsgrad(param, grad, m, v, vhat, lr, step, beta1=0.9, beta2=0.999, eps=1e-7,
+                 grad_scale=1.0):
+    lib().pld_adam_amsgrad(ptr(param), ptr(grad), ptr(m), ptr(v), ptr(vhat), param.numel(),
+                           float(lr), beta1, beta2, eps, int(step), float(grad_scale), stream())
+
+
+# ------------------------------------------------------------------------------------ conv
+def same_pads(h, k, s):
+    """TF 'same' padding: (pad_before, out)."""
+    out = -(-h // s)
+    total = max((out - 1) * s + k - h, 0)
+    return total // 2, out
+
+
+def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None, in_shift=None,
+              in_act="none"):
+    n, h, w, c1 = x1.shape
+    c2 = 0 if x2 is None else x2.shape[3]
+    a = ConvArgs()
+    a.x1 = x1.data_ptr()
+    a.x2 = None if x2 is None else x2.data_ptr()
+    a.c1, a.c2 = c1, c2
+    a.n, a.h, a.w = n, h, w
+    a.kh, a.kw, a.sh, a.sw = kh, kw, stride, stride
+    a.pad_t, a.pad_l = pad_t, pad_l
+    a.oh, a.ow, a.cout = oh, ow, cout
+    a.in_scale = None if in_scale is None else in_scale.data_ptr()
+    a.in_shift = None if in_shift is None else in_shift.data_ptr()
+    a.in_act = ACT[in_act]
+    return a
+
+
+def filter_to_native(w_hwio, out=None):
+    kh, kw, cin, cout = w_hwio.shape
+    out = torch.empty((cout, kh, kw, cin), dtype=torch.float32, device=w_hwio.device) \
+        if out is None else out
+    lib().pld_filter_to_native(ptr(w_hwio), kh, kw, cin, cout, ptr(out), stream())
+    return out
+
+
+def filter_to_dgrad(w_hwio, out=None):
+    kh, kw, cin, cout = w_hwio.shape
+    out = torch.empty((cin, kh, kw, cout), dtype=torch.float32, device=w_hwio.device) \
+        if out is None else out
+    lib().pld_filter_to_dgrad(ptr(w_hwio), kh, kw, cin, cout, ptr(out), stream())
+    return out
+
+
+def conv2d_fwd(args, w_native, bias, y, accumulate=False):
+    lib().pld_conv2d_fwd(C.byref(args), ptr(w_native), ptr(bias), ptr(y), int(accumulate),
+                         stream())
+    return y
+
+
+def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
+    lib().pld_conv2d_dgrad(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(dx1), int(acc1), ptr(dx2),
+                           int(acc2), stream())
+
+
+def conv2d_wgrad(args, dy, dw, accumulate=False):
+    need = lib().pld_conv2d_wgrad_workspace_size(C.byref(args))
+    ws = workspace(need, "wgrad") if need else None
+    lib().pld_conv2d_wgrad(C.byref(args), ptr(dy), ptr(dw), int(accumulate), ptr(ws), need,
+                           stream())
+
+
+def channel_sum(x, rows, c, out, accumulate=False):
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_channel_sum(ptr(x), rows, c, ptr(out), int(accumulate), ptr(ws), stream())
+
+
+# -------------------------------------------------------------------------------------- BN
+def bn_stats(x, rows, c, mean, invstd, moving_mean=None, moving_var=None, eps=1e-3,
+             momentum=0.99):
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_bn_stats(ptr(x), rows, c, eps, momentum, ptr(mean), ptr(invstd), ptr(moving_mean),
+                       ptr(moving_var), ptr(ws), stream())
+
+
+def bn_apply(x, rows, c, mean, invstd, gamma, beta, act, y, gate=None, hw=0):
+    lib().pld_bn_apply(ptr(x), rows, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ACT[act],
+                       ptr(gate), hw, ptr(y), stream())
+
+
+def bn_bwd(x, dy, rows, c, mean, invstd, gamma, beta, act, dx, dgamma, dbeta, gate=None,
+           addn=None, hw=0, dx_accumulate=False, param_accumulate=False):
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_bn_bwd(ptr(x), ptr(dy), rows, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                     ACT[act], ptr(gate), ptr(addn), hw, ptr(dx), int(dx_accumulate),
+                     ptr(dgamma), ptr(dbeta), int(param_accumulate), ptr(ws), stream())
+
+
+def channel_affine_act(x, rows, c, scale, shift, act, y):
+    lib().pld_channel_affine_act(ptr(x), rows, c, ptr(scale), ptr(shift), ACT[act], ptr(y),
+                                 stream())
+
+
+# ------------------------------------------------------------------------------ resampling
+def upsample2x_fwd(x, y):
+    n, h, w, c = x.shape
+    lib().pld_upsample2x_fwd(ptr(x), n, h, w, c, ptr(y), stream())
+    return y
+
+
+def upsample2x_bwd(dy, dx, accumulate=False):
+    n, h, w, c = dx.shape
+    lib().pld_upsample2x_bwd(ptr(dy), n, h, w, c, ptr(dx), int(accumulate), stream())
+    return dx
+
+
+def residual_add(a, sample_scale, b, y):
+    n = a.shape[0]
+    lib().pld_residual_add(ptr(a), ptr(sample_scale), ptr(b), n, a.numel() // n, ptr(y),
+                           stream())
+
+
+def scale_per_sample(x, sample_scale, y, accumulate=False):
+    n = x.shape[0]
+    lib().pld_scale_per_sample(ptr(x), ptr(sample_scale), n, x.numel() // n, ptr(y),
+                               int(accumulate), stream())
+
+
+# ------------------------------------------------------------------------- depthwise / SE
+def dwconv_fwd(x, wdw, k, s, pad_t, pad_l, y):
+    n, h, w, c = x.shape
+    _, oh, ow, _ = y.shape
+    lib().pld_dwconv_fwd(ptr(x), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow, ptr(y),
+                         stream())
+
+
+def dwconv_dgrad(dy, wdw, k, s, pad_t, pad_l, dx, accumulate=False):
+    n, h, w, c = dx.shape
+    _, oh, ow, _ = dy.shape
+    lib().pld_dwconv_dgrad(ptr(dy), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow, ptr(dx),
+                           int(accumulate), stream())
+
+
+def se_fwd(a, w1, b1, w2, b2, pooled, z1, gate):
+    n, h, w, c = a.shape
+    cse = w1.shape[-1]
+    ws = workspace(lib().pld_se_workspace_size(n, h * w, c, cse), "se")
+    lib().pld_se_fwd(ptr(a), n, h * w, c, cse, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(pooled),
+                     ptr(z1), ptr(gate), ptr(ws), stream())
+
+
+def se_bwd(dy, a, w1, w2, z1, gate, addn):
+    n, h, w, c = a.shape
+    cse = w1.shape[-1]
+    ws = workspace(lib().pld_se_workspace_size(n, h * w, c, cse), "se")
+    lib().pld_se_bwd(ptr(dy), ptr(a), n, h * w, c, cse, ptr(w1), ptr(w2), ptr(z1), ptr(gate),
+                     ptr(addn), ptr(ws), stream())
+
+
+# -------------------------------------------------------------------------------- sampler
+def sampler_candidates(R, strategy):
+    return lib().pld_sampler_candidates(R, SAMPLER[strategy])
+
+
+def sampler_compact(mask, gt, valid_idx, nvalid, gt_minmax):
+    B, H, W = mask.shape
+    lib().pld_sampler_compact(ptr(mask), B, H, W, ptr(gt), ptr(valid_idx), ptr(nvalid),
+                              ptr(gt_minmax), None, stream())
+
+
+def sampler_draw(nvalid, n_cand, L, seed, step, image_offset, draws):
+    B = nvalid.shape[0]
+    lib().pld_sampler_draw(ptr(nvalid), B, n_cand, L, seed, step, image_offset, ptr(draws),
+                           stream())
+
+
+def sampler_rank(gt, valid_idx, nvalid, gt_minmax, draws, R, L, strategy, out):
+    B, H, W = gt.shape
+    sid = SAMPLER[strategy]
+    ws = workspace(lib().pld_sampler_workspace_size(B, H, W, R, L, sid), "sampler")
+    lib().pld_sampler_rank(ptr(gt), ptr(valid_idx), ptr(nvalid), ptr(gt_minmax), ptr(draws), B,
+                           H, W, R, L, sid, ptr(out), ptr(ws), stream())
+    return out

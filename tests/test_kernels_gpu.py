@@ -1,0 +1,373 @@
+"""GPU parity tests: every HIP kernel of libpldepth_hip.so against the CPU oracle.
+
+Float kernels are checked against torch-CPU fp64 restatements (oracle/effnet.py helpers) with an
+explicit tolerance; integer/index work (sampler) bit-exactly against oracle/sampler.py fed the
+same draws.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import effnet as OE
+from oracle import listmle as LM
+from oracle import sampler as S
+from pldepth_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3  # BASELINE.json: 1e-3 relative on fp32 activations, loss and gradients
+
+
+def rel_err(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    return float((got - ref).abs().max() / ref.abs().max().clamp(min=1e-30))
+
+
+def dev(t, cuda):
+    return t.to(device=cuda, dtype=torch.float32).contiguous()
+
+
+# ------------------------------------------------------------------------------- ListMLE
+@pytest.mark.parametrize("B,H,W,R,L", [(2, 8, 9, 5, 2), (3, 16, 16, 7, 5), (2, 12, 12, 6, 64),
+                                       (1, 20, 20, 3, 130), (1, 30, 30, 2, 500)])
+def test_listmle_matches_oracle(cuda, B, H, W, R, L):
+    rng = np.random.default_rng(L)
+    pred = rng.standard_normal((B, H, W, 1)).astype(np.float32)
+    idx = rng.integers(0, H * W, (B, R, L))
+    lab = (rng.permutation(B * R * L).reshape(B, R, L) / (B * R * L)).astype(np.float32)
+    lab[0, 0, -1] = -1.0  # an invalid element
+    y = np.stack([idx.astype(np.float32), lab], -1).astype(np.float32)
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred, B, L)
+    loss, dpred, nll = K.listmle_fwd_bwd(dev(torch.from_numpy(pred), cuda),
+                                         dev(torch.from_numpy(y), cuda), B, R, L)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-5
+    assert rel_err(dpred, torch.from_numpy(dpred_ref)) < 1e-5
+
+
+def test_listmle_sorted_input_and_ties_deterministic(cuda):
+    B, H, W, R, L = 2, 10, 10, 4, 5
+    rng = np.random.default_rng(3)
+    pred = rng.standard_normal((B, H, W, 1)).astype(np.float32)
+    idx = rng.integers(0, H * W, (B, R, L))
+    lab = np.sort(rng.integers(0, 4, (B, R, L)) / 4.0, axis=-1)[..., ::-1].astype(np.float32)
+    y = np.ascontiguousarray(np.stack([idx.astype(np.float32), lab], -1))
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred, B, L)
+    loss, dpred, _ = K.listmle_fwd_bwd(dev(torch.from_numpy(pred), cuda),
+                                       dev(torch.from_numpy(y), cuda), B, R, L)
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-5
+    assert rel_err(dpred, torch.from_numpy(dpred_ref)) < 1e-5
+
+
+# ---------------------------------------------------------------------------------- Adam
+def test_adam_amsgrad_matches_oracle(cuda):
+    from oracle.adam import adam_amsgrad_step
+    rng = np.random.default_rng(0)
+    n = 1027
+    p = rng.standard_normal(n).astype(np.float32)
+    st = [np.zeros(n, np.float32) for _ in range(3)]
+    tp = dev(torch.from_numpy(p), cuda)
+    tm, tv, th = (torch.zeros(n, device=cuda) for _ in range(3))
+    for step in range(1, 6):
+        g = rng.standard_normal(n).astype(np.float32) * (0.1 if step % 2 else 3.0)
+        p, *st = adam_amsgrad_step(p, g, *st, lr=0.01, step=step)
+        K.adam_amsgrad(tp, dev(torch.from_numpy(g), cuda), tm, tv, th, lr=0.01, step=step)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(tp.cpu().numpy(), p, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(th.cpu().numpy(), st[2], rtol=1e-5, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------------- conv
+CONV_CASES = [
+    # n, h, w, c1, c2, k, s, cout, bias, prologue
+    (2, 9, 11, 8, 12, 3, 1, 40, True, False),      # decoder-like: 3x3 same + concat
+    (2, 7, 7, 16, 0, 1, 1, 96, False, False),      # 1x1 expand
+    (1, 12, 10, 24, 0, 1, 1, 144, False, False),   # K=24 (not a multiple of 16)
+    (2, 10, 12, 3, 0, 3, 2, 32, False, True),      # stem: Cin=3, s2, asymmetric pad, prologue
+    (2, 16, 16, 32, 0, 3, 1, 1, True, False),      # final conv: Cout=1
+    (1, 14, 14, 64, 64, 3, 1, 130, True, True),    # concat + prologue on source 1
+    (2, 6, 6, 1280, 0, 3, 1, 672, True, False),    # c0-like channel counts
+]
+
+
+def _ref_conv(x1, x2, w, b, k, s, pt, pb, pl, pr, scale=None, shift=None):
+    x = x1
+    if scale is not None:
+        x = torch.relu(x * scale + shift)
+    if x2 is not None:
+        x = torch.cat([x, x2], dim=-1)
+    y = OE.conv(x.permute(0, 3, 1, 2), w, b, s, (pt, pb, pl, pr))
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(cuda, case):
+    n, h, w, c1, c2, k, s, cout, has_bias, pro = case
+    torch.manual_seed(hash(case) % 1000)
+    x1 = torch.randn(n, h, w, c1, dtype=torch.float64)
+    x2 = torch.randn(n, h, w, c2, dtype=torch.float64) if c2 else None
+    wt = torch.randn(k, k, c1 + c2, cout, dtype=torch.float64) / np.sqrt(k * k * (c1 + c2))
+    b = torch.randn(cout, dtype=torch.float64) if has_bias else None
+    scale = torch.rand(c1, dtype=torch.float64) + 0.5 if pro else None
+    shift = torch.randn(c1, dtype=torch.float64) * 0.3 if pro else None
+    if s == 2:
+        pt, pb = OE.correct_pad(h, k)
+        pl, pr = OE.correct_pad(w, k)
+    else:
+        pt, pb, _ = OE.same_pad(h, k, 1)
+        pl, pr, _ = OE.same_pad(w, k, 1)
+    oh = (h + pt + pb - k) // s + 1
+    ow = (w + pl + pr - k) // s + 1
+    x1r = x1.clone().requires_grad_(True)
+    x2r = x2.clone().requires_grad_(True) if x2 is not None else None
+    wr = wt.clone().requires_grad_(True)
+    y_ref = _ref_conv(x1r, x2r, wr, b, k, s, pt, pb, pl, pr, scale, shift)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+
+    gx1, gx2 = dev(x1, cuda), (dev(x2, cuda) if x2 is not None else None)
+    gw = dev(wt, cuda)
+    gsc = dev(scale, cuda) if pro else None
+    gsh = dev(shift, cuda) if pro else None
+    args = K.conv_args(gx1, gx2, k, k, s, pt, pl, oh, ow, cout, gsc, gsh,
+                       "relu" if pro else "none")
+    y = torch.empty(n, oh, ow, cout, device=cuda)
+    K.conv2d_fwd(args, K.filter_to_native(gw), dev(b, cuda) if has_bias else None, y)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
+    # accumulate mode adds onto the destination
+    K.conv2d_fwd(args, K.filter_to_native(gw), dev(b, cuda) if has_bias else None, y,
+                 accumulate=True)
+    assert rel_err(y, 2 * y_ref) < 1e-5
+
+    gdy = dev(dy, cuda)
+    dw = torch.empty(k, k, c1 + c2, cout, device=cuda)
+    K.conv2d_wgrad(args, gdy, dw)
+    torch.cuda.synchronize()
+    assert rel_err(dw, wr.grad) < 1e-5, rel_err(dw, wr.grad)
+
+    if s == 1 and not pro:
+        dx1 = torch.empty_like(gx1)
+        dx2 = torch.full_like(gx2, 1.0) if x2 is not None else None
+        K.conv2d_dgrad(args, gdy, K.filter_to_dgrad(gw), dx1, dx2, acc2=True)
+        torch.cuda.synchronize()
+        assert rel_err(dx1, x1r.grad) < 1e-5, rel_err(dx1, x1r.grad)
+        if x2 is not None:
+            assert rel_err(dx2 - 1.0, x2r.grad) < 1e-5
+
+
+def test_channel_sum(cuda):
+    x = torch.randn(1000, 37, dtype=torch.float64)
+    out = torch.empty(37, device=cuda)
+    K.channel_sum(dev(x, cuda), 1000, 37, out)
+    assert rel_err(out, x.sum(0)) < 1e-6
+    x = torch.randn(5003, 64, dtype=torch.float64)
+    out = torch.ones(64, device=cuda)
+    K.channel_sum(dev(x, cuda), 5003, 64, out, accumulate=True)
+    assert rel_err(out - 1, x.sum(0)) < 1e-5
+
+
+# ------------------------------------------------------------------------------------ BN
+@pytest.mark.parametrize("rows,c,act", [(4096, 32, "relu"), (999, 144, "swish"),
+                                        (300, 1280, "swish"), (50, 6, "none")])
+def test_bn_forward_backward(cuda, rows, c, act):
+    torch.manual_seed(rows + c)
+    x = torch.randn(rows, c, dtype=torch.float64) * 3 + 1.5
+    gamma = torch.rand(c, dtype=torch.float64) + 0.5
+    beta = torch.randn(c, dtype=torch.float64)
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, gamma, beta))
+    mean = xr.mean(0)
+    var = ((xr - mean) ** 2).mean(0)
+    z = (xr - mean) / torch.sqrt(var + 1e-3) * gr + br
+    y_ref = {"relu": torch.relu, "swish": lambda t: t * torch.sigmoid(t),
+             "none": lambda t: t}[act](z)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+
+    gx = dev(x, cuda)
+    gm, gi = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    mm, mv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    K.bn_stats(gx, rows, c, gm, gi, mm, mv)
+    y = torch.empty_like(gx)
+    K.bn_apply(gx, rows, c, gm, gi, dev(gamma, cuda), dev(beta, cuda), act, y)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+    uvar = x.var(0, unbiased=True)
+    assert rel_err(mm, 0.01 * x.mean(0)) < 1e-5
+    assert rel_err(mv, 0.99 + 0.01 * uvar) < 1e-5
+    dx = torch.empty_like(gx)
+    dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd(gx, dev(dy, cuda), rows, c, gm, gi, dev(gamma, cuda), dev(beta, cuda), act, dx, dg,
+             db)
+    torch.cuda.synchronize()
+    assert rel_err(dx, xr.grad) < 1e-4, rel_err(dx, xr.grad)
+    assert rel_err(dg, gr.grad) < 1e-5
+    assert rel_err(db, br.grad) < 1e-5
+
+
+def test_bn_with_se_gate_and_addn(cuda):
+    n, hw, c = 3, 50, 16
+    rows = n * hw
+    torch.manual_seed(5)
+    x = torch.randn(rows, c, dtype=torch.float64)
+    gamma, beta = torch.rand(c, dtype=torch.float64) + .5, torch.randn(c, dtype=torch.float64)
+    gate = torch.rand(n, c, dtype=torch.float64)
+    addn = torch.randn(n, c, dtype=torch.float64) * 0.1
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, gamma, beta))
+    mean = xr.mean(0)
+    var = ((xr - mean) ** 2).mean(0)
+    a = (xr - mean) / torch.sqrt(var + 1e-3) * gr + br
+    a = a * torch.sigmoid(a)
+    y_ref = a.view(n, hw, c) * gate.view(n, 1, c)
+    dy = torch.randn(n, hw, c, dtype=torch.float64)
+    # da = dy*gate + addn (the SE backward contract)
+    (a.view(n, hw, c) * (dy * gate.view(n, 1, c) + addn.view(n, 1, c))).sum().backward()
+    gx = dev(x, cuda)
+    gm, gi = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_stats(gx, rows, c, gm, gi)
+    y = torch.empty_like(gx)
+    K.bn_apply(gx, rows, c, gm, gi, dev(gamma, cuda), dev(beta, cuda), "swish", y,
+               gate=dev(gate, cuda), hw=hw)
+    assert rel_err(y.view(n, hw, c), y_ref) < 1e-5
+    dx = torch.empty_like(gx)
+    dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd(gx, dev(dy.reshape(rows, c), cuda), rows, c, gm, gi, dev(gamma, cuda),
+             dev(beta, cuda), "swish", dx, dg, db, gate=dev(gate, cuda), addn=dev(addn, cuda),
+             hw=hw)
+    torch.cuda.synchronize()
+    assert rel_err(dx, xr.grad) < 1e-4
+    assert rel_err(dg, gr.grad) < 1e-5
+
+
+# ---------------------------------------------------------------------------- resampling
+@pytest.mark.parametrize("n,h,w,c", [(2, 5, 7, 8), (1, 1, 3, 4), (2, 14, 14, 672), (1, 4, 4, 3)])
+def test_upsample2x(cuda, n, h, w, c):
+    x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
+    y_ref = OE.up2(x.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    y = torch.empty(n, 2 * h, 2 * w, c, device=cuda)
+    K.upsample2x_fwd(dev(x.detach(), cuda), y)
+    dx = torch.empty(n, h, w, c, device=cuda)
+    K.upsample2x_bwd(dev(dy, cuda), dx)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-6
+    assert rel_err(dx, x.grad) < 1e-6
+
+
+def test_residual_and_per_sample_scale(cuda):
+    a = torch.randn(3, 4, 5, 8)
+    b = torch.randn(3, 4, 5, 8)
+    sc = torch.tensor([0.0, 1.25, 1.25])
+    y = torch.empty(3, 4, 5, 8, device=cuda)
+    K.residual_add(a.to(cuda), sc.to(cuda), b.to(cuda), y)
+    torch.testing.assert_close(y.cpu(), a * sc.view(3, 1, 1, 1) + b)
+    K.scale_per_sample(a.to(cuda), sc.to(cuda), y, accumulate=True)
+    torch.testing.assert_close(y.cpu(), 2 * a * sc.view(3, 1, 1, 1) + b)
+
+
+# ------------------------------------------------------------------------- depthwise / SE
+@pytest.mark.parametrize("n,h,w,c,k,s", [(2, 12, 12, 16, 3, 1), (2, 12, 10, 24, 3, 2),
+                                         (1, 14, 14, 40, 5, 2), (2, 7, 7, 8, 5, 1),
+                                         (1, 13, 11, 4, 3, 2)])
+def test_dwconv(cuda, n, h, w, c, k, s):
+    torch.manual_seed(k * 10 + s)
+    x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
+    wk = torch.randn(k, k, c, dtype=torch.float64)
+    if s == 2:
+        pt, pb = OE.correct_pad(h, k)
+        pl, pr = OE.correct_pad(w, k)
+    else:
+        pt, pb, _ = OE.same_pad(h, k, 1)
+        pl, pr, _ = OE.same_pad(w, k, 1)
+    y_ref = OE.dwconv(x.permute(0, 3, 1, 2), wk, s, (pt, pb, pl, pr)).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    oh, ow = y_ref.shape[1:3]
+    y = torch.empty(n, oh, ow, c, device=cuda)
+    K.dwconv_fwd(dev(x.detach(), cuda), dev(wk, cuda), k, s, pt, pl, y)
+    dx = torch.empty(n, h, w, c, device=cuda)
+    K.dwconv_dgrad(dev(dy, cuda), dev(wk, cuda), k, s, pt, pl, dx)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+    assert rel_err(dx, x.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n,h,w,c,cse", [(2, 6, 6, 96, 4), (3, 14, 14, 1152, 48),
+                                         (1, 2, 2, 16, 8)])
+def test_se_fwd_bwd(cuda, n, h, w, c, cse):
+    torch.manual_seed(c)
+    a = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
+    w1 = torch.randn(1, 1, c, cse, dtype=torch.float64) * 0.2
+    b1 = torch.randn(cse, dtype=torch.float64) * 0.1
+    w2 = torch.randn(1, 1, cse, c, dtype=torch.float64) * 0.2
+    b2 = torch.randn(c, dtype=torch.float64) * 0.1
+    an = a.permute(0, 3, 1, 2)
+    pooled = an.mean(dim=(2, 3), keepdim=True)
+    z1 = OE.conv(pooled, w1, b1)
+    gate = torch.sigmoid(OE.conv(OE.swish(z1), w2, b2))
+    y_ref = (an * gate).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    ga = dev(a.detach(), cuda)
+    gp, gz, gg = (torch.empty(n, c, device=cuda), torch.empty(n, cse, device=cuda),
+                  torch.empty(n, c, device=cuda))
+    K.se_fwd(ga, dev(w1.view(c, cse), cuda), dev(b1, cuda), dev(w2.view(cse, c), cuda),
+             dev(b2, cuda), gp, gz, gg)
+    torch.cuda.synchronize()
+    assert rel_err(gg, gate.view(n, c)) < 1e-5
+    addn = torch.empty(n, c, device=cuda)
+    gdy = dev(dy, cuda)
+    K.se_bwd(gdy, ga, dev(w1.view(c, cse), cuda), dev(w2.view(cse, c), cuda), gz, gg, addn)
+    torch.cuda.synchronize()
+    da = gdy * gg.view(n, 1, 1, c) + addn.view(n, 1, 1, c)
+    assert rel_err(da, a.grad) < 1e-4
+
+
+# ------------------------------------------------------------------------------- sampler
+@pytest.mark.parametrize("ci", range(4))
+@pytest.mark.parametrize("strategy", ["thresh", "info", "pure", "masked"])
+def test_sampler_bit_exact_vs_oracle(cuda, golden, ci, strategy):
+    h, w, L, R = [int(v) for v in golden[f"c{ci}_shape"]]
+    mask = np.unpackbits(golden[f"c{ci}_mask"])[: h * w].reshape(h, w).astype(np.float32)
+    gt = golden[f"c{ci}_codes"].astype(np.float32) / np.float32(255)
+    draws = golden[f"c{ci}_{strategy}_draws"].astype(np.int32)
+    ref, _ = S.sample_masked_point_batch(strategy, mask, gt, R, L, draws)
+    B = 2  # two copies of the image: per-image indexing
+    gmask = dev(torch.from_numpy(np.stack([mask, mask])), cuda)
+    ggt = dev(torch.from_numpy(np.stack([gt, gt])), cuda)
+    vi = torch.empty(B, h * w, dtype=torch.int32, device=cuda)
+    nv = torch.empty(B, dtype=torch.int32, device=cuda)
+    mm = torch.empty(B, 2, device=cuda)
+    K.sampler_compact(gmask, ggt, vi, nv, mm)
+    gd = torch.from_numpy(np.stack([draws, draws])).to(cuda).contiguous()
+    out = torch.empty((B,) + ref.shape, device=cuda)
+    K.sampler_rank(ggt, vi, nv, mm, gd, R, L, strategy, out)
+    torch.cuda.synchronize()
+    assert nv.cpu().tolist() == [int(mask.sum())] * 2
+    for b in range(B):
+        np.testing.assert_array_equal(out[b].cpu().numpy(), ref)
+
+
+def test_sampler_draws_uniform_and_in_range(cuda):
+    B, n_cand, L = 4, 500, 5
+    nv = torch.tensor([1, 7, 1000, 200000], dtype=torch.int32, device=cuda)
+    d = torch.empty(B, n_cand, L, dtype=torch.int32, device=cuda)
+    K.sampler_draw(nv, n_cand, L, seed=1234, step=7, image_offset=0, draws=d)
+    d2 = torch.empty_like(d)
+    K.sampler_draw(nv, n_cand, L, seed=1234, step=7, image_offset=0, draws=d2)
+    d3 = torch.empty_like(d)
+    K.sampler_draw(nv, n_cand, L, seed=1234, step=8, image_offset=0, draws=d3)
+    torch.cuda.synchronize()
+    d, d2, d3 = d.cpu(), d2.cpu(), d3.cpu()
+    assert torch.equal(d, d2) and not torch.equal(d, d3)
+    for b, n in enumerate([1, 7, 1000, 200000]):
+        assert int(d[b].min()) >= 0 and int(d[b].max()) < n
+    counts = torch.bincount(d[1].flatten(), minlength=7).double()
+    exp = n_cand * L / 7
+    assert float(((counts - exp) ** 2 / exp).sum()) < 30  # chi2, 6 dof
+    # image_offset makes draws independent of the shard layout
+    e = torch.empty(2, n_cand, L, dtype=torch.int32, device=cuda)
+    K.sampler_draw(nv[2:].contiguous(), n_cand, L, seed=1234, step=7, image_offset=2, draws=e)
+    assert torch.equal(e.cpu(), d[2:])
