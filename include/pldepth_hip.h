@@ -141,6 +141,12 @@ int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float
                const float* gate, const float* addn, int hw, float* dx, int dx_accumulate,
                float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
 
+/* inference-mode BN (Keras BatchNormalization, training=False): scale = gamma/sqrt(mvar+eps),
+ * shift = beta - mmean*scale, for pld_channel_affine_act / the conv prologue */
+int pld_bn_inference_coeffs(const float* gamma, const float* beta, const float* moving_mean,
+                            const float* moving_var, int c, float eps, float* scale, float* shift,
+                            void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Elementwise / resampling
  * ------------------------------------------------------------------------------------------ */
@@ -156,6 +162,11 @@ int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx, i
  * residual add); sample_scale may be NULL (=1). rows_per_img*c elements per image. */
 int pld_residual_add(const float* a, const float* sample_scale, const float* b, int n,
                      int64_t elems_per_img, float* y, void* stream);
+/* Dropout(rate, noise_shape=(N,1,1,1)) keep factors for drop-connect: scales[i] = keep ? 1/(1-rate)
+ * : 0 with keep ~ Bernoulli(1-rate) from Philox4x32-10 keyed by (seed), counter (layer,
+ * image_offset+i, step). */
+int pld_dropconnect_scales(float* scales, int n, float rate, uint64_t seed, uint64_t step,
+                           int layer, int image_offset, void* stream);
 /* y[i] = x[i] * sample_scale[img] (+ y[i] when accumulate) */
 int pld_scale_per_sample(const float* x, const float* sample_scale, int n, int64_t elems_per_img,
                          float* y, int accumulate, void* stream);

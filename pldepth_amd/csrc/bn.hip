@@ -336,9 +336,29 @@ static size_t red_ws_doubles(long rows, int C) {
   return (size_t)nbx * C * 2;
 }
 
+__global__ void bn_infer_kernel(const float* __restrict__ g, const float* __restrict__ b,
+                                const float* __restrict__ mm, const float* __restrict__ mv, int c,
+                                float eps, float* __restrict__ sc, float* __restrict__ sh) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  const float s = g[i] / sqrtf(mv[i] + eps);
+  sc[i] = s;
+  sh[i] = b[i] - mm[i] * s;
+}
+
 }  // namespace pld
 
 using namespace pld;
+
+extern "C" int pld_bn_inference_coeffs(const float* gamma, const float* beta,
+                                       const float* moving_mean, const float* moving_var, int c,
+                                       float eps, float* scale, float* shift, void* stream) {
+  PLD_CHECK_ARG(gamma && beta && moving_mean && moving_var && scale && shift && c > 0,
+                "pld_bn_inference_coeffs: bad args");
+  bn_infer_kernel<<<cdiv(c, 256), 256, 0, as_stream(stream)>>>(gamma, beta, moving_mean,
+                                                                moving_var, c, eps, scale, shift);
+  return check_launch("bn_infer_kernel");
+}
 
 extern "C" size_t pld_channel_reduce_workspace_size(int64_t rows, int c) {
   if (rows <= 0 || c <= 0) return 0;

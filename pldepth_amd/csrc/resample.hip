@@ -148,6 +148,25 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
   }
 }
 
+__global__ void dropconnect_kernel(float* __restrict__ sc, int n, float rate, uint64_t seed,
+                                   uint64_t step, int layer, int off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint4 c = make_uint4((uint32_t)layer, (uint32_t)(off + i), (uint32_t)step,
+                       (uint32_t)(step >> 32) ^ 0x5D0Cu);
+  uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {  // Philox4x32-10
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  const float u = (float)(c.x >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+  sc[i] = (u >= rate) ? 1.0f / (1.0f - rate) : 0.0f;
+}
+
 static unsigned grid_for(long n) { return std::min<unsigned>(std::max(cdiv(n, 256), 1u), 8192); }
 
 }  // namespace pld
@@ -185,6 +204,14 @@ extern "C" int pld_residual_add(const float* a, const float* sample_scale, const
   residual_kernel<<<grid_for(total), 256, 0, as_stream(stream)>>>(a, sample_scale, b,
                                                                   elems_per_img, total, y, 0);
   return check_launch("residual_kernel");
+}
+
+extern "C" int pld_dropconnect_scales(float* scales, int n, float rate, uint64_t seed,
+                                      uint64_t step, int layer, int image_offset, void* stream) {
+  PLD_CHECK_ARG(scales && n > 0 && rate >= 0.f && rate < 1.f, "pld_dropconnect_scales: bad args");
+  dropconnect_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(scales, n, rate, seed, step,
+                                                                  layer, image_offset);
+  return check_launch("dropconnect_kernel");
 }
 
 extern "C" int pld_scale_per_sample(const float* x, const float* sample_scale, int n,

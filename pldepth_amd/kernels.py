@@ -171,6 +171,16 @@ def residual_add(a, sample_scale, b, y):
                            stream())
 
 
+def dropconnect_scales(scales, rate, seed, step, layer, image_offset=0):
+    lib().pld_dropconnect_scales(ptr(scales), scales.numel(), float(rate), seed, step, layer,
+                                 image_offset, stream())
+
+
+def bn_inference_coeffs(gamma, beta, mmean, mvar, scale, shift, eps=1e-3):
+    lib().pld_bn_inference_coeffs(ptr(gamma), ptr(beta), ptr(mmean), ptr(mvar), gamma.numel(),
+                                  eps, ptr(scale), ptr(shift), stream())
+
+
 def scale_per_sample(x, sample_scale, y, accumulate=False):
     n = x.shape[0]
     lib().pld_scale_per_sample(ptr(x), ptr(sample_scale), n, x.numel() // n, ptr(y),

@@ -1,0 +1,604 @@
+"""ff_effnet on MI355X: EfficientNetB0 encoder (frozen convs, trainable BN) + the PLDepth decoder.
+
+Replaces the Keras graph built by ``EffNetFullyFledged.get_model_and_normalization``
+(pldepth/models/pl_hourglass.py:45-100) and the TF kernels Keras dispatches for its forward and
+backward passes. Every FLOP runs in libpldepth_hip.so; this module only owns device buffers,
+orders the launches on one stream and names parameters after the Keras layers (so weights map
+1:1 to the reference's ``model.get_weights()`` layout: Conv2D kernels HWIO, depthwise
+[k][k][c], BN gamma/beta/moving_mean/moving_variance).
+
+Data layout in HBM (one replica):
+  * ``params``  flat fp32, every trainable tensor (decoder conv kernels + biases, all 54 BN
+                gamma/beta) — the Adam / all-reduce unit; ``grads``, Adam m, v, vhat alike;
+  * ``frozen``  flat fp32, encoder conv / depthwise / SE weights and the input normalisation;
+  * ``stats``   flat fp32, BN moving mean / variance;
+  * native copies of every conv filter ([cout][kh][kw][cin] forward, flipped [cin][kh][kw][cout]
+    for dX), refreshed after each optimizer step for the trainable (decoder) filters;
+  * activations NHWC fp32: every pre-BN tensor is kept for the backward pass (BN and its
+    activation are re-applied from it), plus the post-activation tensors the next op reads.
+"""
+import math
+
+import numpy as np
+import torch
+
+from .. import kernels as K
+
+BN_EPS = 1e-3
+BN_MOMENTUM = 0.99
+# keras.applications.efficientnet DEFAULT_BLOCKS_ARGS (B0): kernel, repeats, in, out, expand, stride
+B0_BLOCKS = [
+    (3, 1, 32, 16, 1, 1),
+    (3, 2, 16, 24, 6, 2),
+    (5, 2, 24, 40, 6, 2),
+    (3, 3, 40, 80, 6, 2),
+    (5, 3, 80, 112, 6, 1),
+    (5, 4, 112, 192, 6, 2),
+    (3, 1, 192, 320, 6, 1),
+]
+DROP_CONNECT_RATE = 0.2
+# decoder (pl_hourglass.py:59-96): conv name, cout, skip concatenated after the x2 upsampling
+DECODER = [
+    ("dec_conv0", 672, "block6a_expand_activation"),
+    ("dec_conv1", 240, "block4a_expand_activation"),
+    ("dec_conv2", 144, "block3a_expand_activation"),
+    ("dec_conv3", 32, None),
+    ("dec_conv4", 32, None),
+]
+# Keras' EfficientNet ImageNet checkpoint (TF 2.3-2.8) stores these in its Normalization layer
+IMAGENET_MEAN = [0.485, 0.456, 0.406]
+IMAGENET_VARIANCE = [0.229, 0.224, 0.225]
+
+
+def block_specs():
+    """(name, kernel, stride, filters_in, filters_out, expand_ratio, drop_rate) per block, as
+    keras.applications.efficientnet.EfficientNet expands DEFAULT_BLOCKS_ARGS."""
+    out, b = [], 0
+    total = float(sum(r for _, r, *_ in B0_BLOCKS))
+    for i, (k, reps, fin, fout, ex, s) in enumerate(B0_BLOCKS):
+        for j in range(reps):
+            out.append((f"block{i + 1}{chr(97 + j)}_", k, s if j == 0 else 1,
+                        fin if j == 0 else fout, fout, ex, DROP_CONNECT_RATE * b / total))
+            b += 1
+    return out
+
+
+def correct_pad(size, k):
+    """keras imagenet_utils.correct_pad -> (before, after) for one spatial dim."""
+    adjust = 1 - size % 2
+    return k // 2 - adjust, k // 2
+
+
+def same_pad(size, k, s):
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return total // 2, out
+
+
+class FlatStore:
+    """Named views into one flat fp32 device buffer (16-byte aligned segments)."""
+
+    def __init__(self):
+        self.specs = []  # (name, shape, offset)
+        self.size = 0
+        self.buf = None
+        self.views = {}
+
+    def add(self, name, shape):
+        n = int(np.prod(shape))
+        self.specs.append((name, tuple(shape), self.size))
+        self.size += (n + 3) // 4 * 4
+        return name
+
+    def materialize(self, device):
+        self.buf = torch.zeros(max(self.size, 4), dtype=torch.float32, device=device)
+        for name, shape, off in self.specs:
+            n = int(np.prod(shape))
+            self.views[name] = self.buf[off:off + n].view(shape)
+        return self
+
+    def like(self):
+        t = FlatStore()
+        t.specs, t.size = self.specs, self.size
+        return t
+
+    def __getitem__(self, name):
+        return self.views[name]
+
+    def names(self):
+        return [s[0] for s in self.specs]
+
+
+class _BN:
+    def __init__(self, eng, name, c):
+        self.name, self.c = name, c
+        self.g = eng.params.add(name + "/gamma", (c,))
+        self.b = eng.params.add(name + "/beta", (c,))
+        self.mm = eng.stats.add(name + "/moving_mean", (c,))
+        self.mv = eng.stats.add(name + "/moving_variance", (c,))
+        eng.bns.append(self)
+
+    def bind(self, eng):
+        dev = eng.device
+        self.gamma, self.beta = eng.params[self.g], eng.params[self.b]
+        self.dgamma, self.dbeta = eng.grads[self.g], eng.grads[self.b]
+        self.mmean, self.mvar = eng.stats[self.mm], eng.stats[self.mv]
+        self.mean = torch.empty(self.c, device=dev)
+        self.invstd = torch.empty(self.c, device=dev)
+        self.inf_scale = torch.empty(self.c, device=dev)
+        self.inf_shift = torch.empty(self.c, device=dev)
+
+    def stats_(self, x, rows, training):
+        if training:
+            K.bn_stats(x, rows, self.c, self.mean, self.invstd, self.mmean, self.mvar, BN_EPS,
+                       BN_MOMENTUM)
+        else:
+            K.bn_inference_coeffs(self.gamma, self.beta, self.mmean, self.mvar, self.inf_scale,
+                                  self.inf_shift, BN_EPS)
+
+    def apply(self, x, rows, act, y, training, gate=None, hw=0):
+        if training:
+            K.bn_apply(x, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, act, y,
+                       gate=gate, hw=hw)
+        else:
+            assert gate is None
+            K.channel_affine_act(x, rows, self.c, self.inf_scale, self.inf_shift, act, y)
+
+    def bwd(self, x, dy, rows, act, dx, dx_acc=False, gate=None, addn=None, hw=0):
+        K.bn_bwd(x, dy, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, act, dx,
+                 self.dgamma, self.dbeta, gate=gate, addn=addn, hw=hw, dx_accumulate=dx_acc)
+
+
+class _Conv:
+    def __init__(self, eng, name, k, cin, cout, stride=1, bias=False, trainable=False,
+                 need_dgrad=True):
+        self.name, self.k, self.cin, self.cout, self.stride = name, k, cin, cout, stride
+        self.has_bias, self.trainable, self.need_dgrad = bias, trainable, need_dgrad
+        store = eng.params if trainable else eng.frozen
+        self.wk = store.add(name + "/kernel", (k, k, cin, cout))
+        self.bk = store.add(name + "/bias", (cout,)) if bias else None
+        eng.convs.append(self)
+
+    def bind(self, eng):
+        store = eng.params if self.trainable else eng.frozen
+        self.w = store[self.wk]
+        self.b = store[self.bk] if self.bk else None
+        if self.trainable:
+            self.dw = eng.grads[self.wk]
+            self.db = eng.grads[self.bk] if self.bk else None
+        dev = eng.device
+        self.w_nat = torch.empty(self.cout, self.k, self.k, self.cin, device=dev)
+        self.w_dg = (torch.empty(self.cin, self.k, self.k, self.cout, device=dev)
+                     if self.need_dgrad else None)
+
+    def refresh(self):
+        K.filter_to_native(self.w, self.w_nat)
+        if self.w_dg is not None:
+            K.filter_to_dgrad(self.w, self.w_dg)
+
+
+class EffNetFF:
+    """Keras-named parameters + buffers + launch order of one ff_effnet replica."""
+
+    def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0):
+        H, W, C = input_shape
+        assert C == 3 and H % 32 == 0 and W % 32 == 0, "input must be RGB with H, W % 32 == 0"
+        self.H, self.W, self.B = H, W, batch_size
+        self.device = torch.device(device)
+        self.params, self.frozen, self.stats = FlatStore(), FlatStore(), FlatStore()
+        self.bns, self.convs = [], []
+        self._build_spec()
+        self.params.materialize(self.device)
+        self.grads = self.params.like().materialize(self.device)
+        self.frozen.materialize(self.device)
+        self.stats.materialize(self.device)
+        for m in self.bns + self.convs:
+            m.bind(self)
+        self.norm_scale = torch.empty(3, device=self.device)
+        self.norm_shift = torch.empty(3, device=self.device)
+        self.init_weights(seed)
+        self._alloc_activations()
+        self.drop_connect = True
+        self.seed = seed
+
+    # ------------------------------------------------------------------ graph structure
+    def _build_spec(self):
+        f = self.frozen
+        f.add("normalization/mean", (3,))
+        f.add("normalization/variance", (3,))
+        self.stem = _Conv(self, "stem_conv", 3, 3, 32, stride=2, need_dgrad=False)
+        self.stem_bn = _BN(self, "stem_bn", 32)
+        self.blocks = []
+        for name, k, s, cin, cout, ex, rate in block_specs():
+            cexp = cin * ex
+            cse = max(1, int(cin * 0.25))
+            blk = dict(name=name, k=k, s=s, cin=cin, cout=cout, ex=ex, rate=rate, cexp=cexp,
+                       cse=cse, residual=(s == 1 and cin == cout))
+            if ex != 1:
+                blk["expand"] = _Conv(self, name + "expand_conv", 1, cin, cexp)
+                blk["expand_bn"] = _BN(self, name + "expand_bn", cexp)
+            blk["dw"] = f.add(name + "dwconv/depthwise_kernel", (k, k, cexp))
+            blk["bn"] = _BN(self, name + "bn", cexp)
+            blk["se_w1"] = f.add(name + "se_reduce/kernel", (1, 1, cexp, cse))
+            blk["se_b1"] = f.add(name + "se_reduce/bias", (cse,))
+            blk["se_w2"] = f.add(name + "se_expand/kernel", (1, 1, cse, cexp))
+            blk["se_b2"] = f.add(name + "se_expand/bias", (cexp,))
+            blk["project"] = _Conv(self, name + "project_conv", 1, cexp, cout)
+            blk["project_bn"] = _BN(self, name + "project_bn", cout)
+            self.blocks.append(blk)
+        self.top = _Conv(self, "top_conv", 1, 320, 1280)
+        self.top_bn = _BN(self, "top_bn", 1280)
+        self.dec = []
+        cin = 1280
+        skip_c = {"block6a_expand_activation": 672, "block4a_expand_activation": 240,
+                  "block3a_expand_activation": 144}
+        for i, (name, cout, skip) in enumerate(DECODER):
+            conv = _Conv(self, name, 3, cin, cout, bias=True, trainable=True)
+            bn = _BN(self, f"dec_bn{i}", cout)
+            self.dec.append((conv, bn, skip))
+            cin = cout + (skip_c[skip] if skip else 0)
+        self.final = _Conv(self, "dec_conv5", 3, 32, 1, bias=True, trainable=True)
+
+    # ------------------------------------------------------------------ weights
+    def init_weights(self, seed=0):
+        """Keras default initialisers (ImageNet weights are a network download the reference
+        makes at pl_hourglass.py:48; unavailable offline): EfficientNet convs
+        VarianceScaling(2.0, fan_out, truncated_normal), decoder Conv2D glorot_uniform, zero
+        biases, BN gamma=1 beta=0 mean=0 var=1, ImageNet normalisation constants."""
+        rng = np.random.default_rng(seed)
+        host = {}
+
+        def trunc_normal(shape, std):
+            v = rng.standard_normal(int(np.prod(shape)))
+            bad = np.abs(v) > 2
+            while bad.any():
+                v[bad] = rng.standard_normal(int(bad.sum()))
+                bad = np.abs(v) > 2
+            return (v * std).reshape(shape)
+
+        def vs_fan_out(shape, depthwise=False):
+            k = shape[0] * shape[1]
+            fan_out = k * (1 if depthwise else shape[-1])
+            return trunc_normal(shape, math.sqrt(2.0 / fan_out) / 0.87962566103423978)
+
+        for name, shape, _ in self.frozen.specs:
+            if name == "normalization/mean":
+                host[name] = np.array(IMAGENET_MEAN)
+            elif name == "normalization/variance":
+                host[name] = np.array(IMAGENET_VARIANCE)
+            elif name.endswith("/bias"):
+                host[name] = np.zeros(shape)
+            elif name.endswith("depthwise_kernel"):
+                host[name] = vs_fan_out(shape + (1,), depthwise=True).reshape(shape)
+            else:
+                host[name] = vs_fan_out(shape)
+        for name, shape, _ in self.params.specs:
+            if name.endswith("/gamma"):
+                host[name] = np.ones(shape)
+            elif name.endswith("/beta") or name.endswith("/bias"):
+                host[name] = np.zeros(shape)
+            else:  # decoder conv kernels: glorot_uniform
+                rf = shape[0] * shape[1]
+                lim = math.sqrt(6.0 / (rf * shape[2] + rf * shape[3]))
+                host[name] = rng.uniform(-lim, lim, shape)
+        for name, shape, _ in self.stats.specs:
+            host[name] = np.ones(shape) if name.endswith("variance") else np.zeros(shape)
+        self.set_weights(host)
+
+    def get_weights(self):
+        """{keras_name: numpy float32} for every parameter, frozen weight and BN statistic."""
+        out = {}
+        for store in (self.params, self.frozen, self.stats):
+            for name in store.names():
+                out[name] = store[name].detach().cpu().numpy().copy()
+        return out
+
+    def set_weights(self, weights):
+        for store in (self.params, self.frozen, self.stats):
+            for name, shape, _ in store.specs:
+                if name in weights:
+                    store[name].copy_(torch.as_tensor(np.asarray(weights[name], np.float32)
+                                                      .reshape(shape)))
+        self.refresh_frozen()
+        self.refresh_trainable()
+
+    def refresh_frozen(self):
+        for c in self.convs:
+            if not c.trainable:
+                c.refresh()
+        # Rescaling(1/255) + Normalization folded into the stem conv's input prologue
+        mean = self.frozen["normalization/mean"].double().cpu()
+        var = self.frozen["normalization/variance"].double().cpu()
+        sd = torch.clamp(torch.sqrt(var), min=1e-7)
+        self.norm_scale.copy_((1.0 / (255.0 * sd)).float())
+        self.norm_shift.copy_((-mean / sd).float())
+
+    def refresh_trainable(self):
+        for c in self.convs:
+            if c.trainable:
+                c.refresh()
+
+    # ------------------------------------------------------------------ activations
+    def _alloc_activations(self):
+        B, H, W = self.B, self.H, self.W
+        dev = self.device
+        self.act, self.gact = {}, {}
+
+        def new(name, shape, grad=True):
+            self.act[name] = torch.empty(shape, device=dev)
+            if grad:
+                self.gact[name] = torch.empty(shape, device=dev)
+
+        new("input", (B, H, W, 3), grad=False)
+        h, w = H // 2, W // 2
+        new("stem_pre", (B, h, w, 32), grad=False)
+        new("stem_activation", (B, h, w, 32))
+        for blk in self.blocks:
+            n, k, s, cexp, cout = blk["name"], blk["k"], blk["s"], blk["cexp"], blk["cout"]
+            blk["h"], blk["w"] = h, w
+            if blk["ex"] != 1:
+                new(n + "expand_pre", (B, h, w, cexp), grad=False)
+                new(n + "expand_activation", (B, h, w, cexp))
+            if s == 2:
+                pt, _ = correct_pad(h, k)
+                pl, _ = correct_pad(w, k)
+                oh, ow = h // 2, w // 2
+            else:
+                pt, oh = same_pad(h, k, 1)
+                pl, ow = same_pad(w, k, 1)
+            blk["pad"], blk["oh"], blk["ow"] = (pt, pl), oh, ow
+            new(n + "dw_pre", (B, oh, ow, cexp), grad=False)
+            new(n + "activation", (B, oh, ow, cexp))      # swish(bn(dw)) (SE input)
+            new(n + "se_excite", (B, oh, ow, cexp))       # activation * gate
+            new(n + "project_pre", (B, oh, ow, cout), grad=False)
+            new(n + "output", (B, oh, ow, cout))
+            blk["pooled"] = torch.empty(B, cexp, device=dev)
+            blk["z1"] = torch.empty(B, blk["cse"], device=dev)
+            blk["gate"] = torch.empty(B, cexp, device=dev)
+            blk["addn"] = torch.empty(B, cexp, device=dev)
+            blk["drop"] = torch.ones(B, device=dev)
+            blk["dbn"] = torch.empty(B, oh, ow, cout, device=dev) if blk["residual"] else None
+            h, w = oh, ow
+        new("top_pre", (B, h, w, 1280), grad=False)
+        new("top_activation", (B, h, w, 1280))
+        for i, (conv, bn, skip) in enumerate(self.dec):
+            new(f"dec{i}_pre", (B, h, w, conv.cout), grad=False)
+            new(f"dec{i}_act", (B, h, w, conv.cout))
+            h, w = 2 * h, 2 * w
+            new(f"dec{i}_up", (B, h, w, conv.cout))
+        new("pred", (B, H, W, 1))
+        # pre-BN gradient scratch, one per distinct shape
+        self._gpre = {}
+
+    def _gpre_buf(self, shape):
+        key = tuple(shape)
+        if key not in self._gpre:
+            self._gpre[key] = torch.empty(key, device=self.device)
+        return self._gpre[key]
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, training=True, step=0):
+        A = self.act
+        B = self.B
+        a = K.conv_args
+        # stem: normalisation prologue, TF-SAME stride-2 (correct_pad) conv, BN, swish
+        pt, _ = correct_pad(self.H, 3)
+        pl, _ = correct_pad(self.W, 3)
+        x = A["input"]
+        h, w = self.H // 2, self.W // 2
+        args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none")
+        K.conv2d_fwd(args, self.stem.w_nat, None, A["stem_pre"])
+        rows = B * h * w
+        self.stem_bn.stats_(A["stem_pre"], rows, training)
+        self.stem_bn.apply(A["stem_pre"], rows, "swish", A["stem_activation"], training)
+        x = A["stem_activation"]
+        for li, blk in enumerate(self.blocks):
+            x = self._block_fwd(blk, x, training, step, li)
+        h, w = x.shape[1], x.shape[2]
+        rows = B * h * w
+        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280), self.top.w_nat, None, A["top_pre"])
+        self.top_bn.stats_(A["top_pre"], rows, training)
+        self.top_bn.apply(A["top_pre"], rows, "swish", A["top_activation"], training)
+        x, x2 = A["top_activation"], None
+        for i, (conv, bn, skip) in enumerate(self.dec):
+            pt, _ = same_pad(h, 3, 1)
+            pl, _ = same_pad(w, 3, 1)
+            args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout)
+            K.conv2d_fwd(args, conv.w_nat, conv.b, A[f"dec{i}_pre"])
+            rows = B * h * w
+            bn.stats_(A[f"dec{i}_pre"], rows, training)
+            bn.apply(A[f"dec{i}_pre"], rows, "relu", A[f"dec{i}_act"], training)
+            K.upsample2x_fwd(A[f"dec{i}_act"], A[f"dec{i}_up"])
+            h, w = 2 * h, 2 * w
+            x, x2 = A[f"dec{i}_up"], (A[skip] if skip else None)
+        pt, _ = same_pad(h, 3, 1)
+        pl, _ = same_pad(w, 3, 1)
+        K.conv2d_fwd(a(x, None, 3, 3, 1, pt, pl, h, w, 1), self.final.w_nat, self.final.b,
+                     A["pred"])
+        return A["pred"]
+
+    def _block_fwd(self, blk, x, training, step, li):
+        A, B, n = self.act, self.B, blk["name"]
+        h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
+        if blk["ex"] != 1:
+            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"]),
+                         blk["expand"].w_nat, None, A[n + "expand_pre"])
+            blk["expand_bn"].stats_(A[n + "expand_pre"], B * h * w, training)
+            blk["expand_bn"].apply(A[n + "expand_pre"], B * h * w, "swish",
+                                   A[n + "expand_activation"], training)
+            e = A[n + "expand_activation"]
+        else:
+            e = x
+        pt, pl = blk["pad"]
+        K.dwconv_fwd(e, self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl, A[n + "dw_pre"])
+        rows = B * oh * ow
+        bn = blk["bn"]
+        bn.stats_(A[n + "dw_pre"], rows, training)
+        bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
+        F = self.frozen
+        K.se_fwd(A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
+                 F[blk["se_b1"]], F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]],
+                 blk["pooled"], blk["z1"], blk["gate"])
+        if training:
+            bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "se_excite"], True, gate=blk["gate"],
+                     hw=oh * ow)
+        else:
+            self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
+        K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"]),
+                     blk["project"].w_nat, None, A[n + "project_pre"])
+        pbn = blk["project_bn"]
+        pbn.stats_(A[n + "project_pre"], rows, training)
+        out = A[n + "output"]
+        pbn.apply(A[n + "project_pre"], rows, "none", out, training)
+        if blk["residual"]:
+            drop = None
+            if training and self.drop_connect and blk["rate"] > 0:
+                K.dropconnect_scales(blk["drop"], blk["rate"], self.seed, step, li)
+                drop = blk["drop"]
+            K.residual_add(out, drop, x, out)
+        return out
+
+    def _gate_mul(self, a, gate, y):
+        """inference path: y = a * gate[img][c] (a BN apply with identity statistics is exact:
+        ((a - 0) * 1) * 1 + 0 = a, then * gate)."""
+        c = a.shape[-1]
+        if not hasattr(self, "_ident"):
+            self._ident = {}
+        if c not in self._ident:
+            self._ident[c] = (torch.zeros(c, device=self.device),
+                              torch.ones(c, device=self.device))
+        z, o = self._ident[c]
+        K.bn_apply(a, a.numel() // c, c, z, o, o, z, "none", y, gate=gate,
+                   hw=a.shape[1] * a.shape[2])
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dpred):
+        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params)."""
+        A, G, B = self.act, self.gact, self.B
+        a = K.conv_args
+        h, w = self.H, self.W
+        # final conv (bias, no BN)
+        pt, _ = same_pad(h, 3, 1)
+        pl, _ = same_pad(w, 3, 1)
+        x4 = A["dec4_up"]
+        args = a(x4, None, 3, 3, 1, pt, pl, h, w, 1)
+        K.conv2d_wgrad(args, dpred, self.final.dw)
+        K.channel_sum(dpred, B * h * w, 1, self.final.db)
+        K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
+        for i in range(len(self.dec) - 1, -1, -1):
+            conv, bn, skip = self.dec[i]
+            h, w = h // 2, w // 2
+            K.upsample2x_bwd(G[f"dec{i}_up"], G[f"dec{i}_act"])
+            rows = B * h * w
+            gpre = self._gpre_buf(A[f"dec{i}_pre"].shape)
+            bn.bwd(A[f"dec{i}_pre"], G[f"dec{i}_act"], rows, "relu", gpre)
+            if i == 0:
+                x1, x2, g1, g2 = A["top_activation"], None, G["top_activation"], None
+            else:
+                pconv, _, pskip = self.dec[i - 1]
+                x1 = A[f"dec{i - 1}_up"]
+                x2 = A[pskip] if pskip else None
+                g1, g2 = G[f"dec{i - 1}_up"], (G[pskip] if pskip else None)
+            pt, _ = same_pad(h, 3, 1)
+            pl, _ = same_pad(w, 3, 1)
+            args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout)
+            K.conv2d_wgrad(args, gpre, conv.dw)
+            K.channel_sum(gpre, rows, conv.cout, conv.db)
+            K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
+        # encoder
+        h, w = A["top_pre"].shape[1:3]
+        rows = B * h * w
+        gpre = self._gpre_buf(A["top_pre"].shape)
+        self.top_bn.bwd(A["top_pre"], G["top_activation"], rows, "swish", gpre)
+        last = self.blocks[-1]["name"] + "output"
+        K.conv2d_dgrad(a(A[last], None, 1, 1, 1, 0, 0, h, w, 1280), gpre, self.top.w_dg, G[last])
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            blk = self.blocks[bi]
+            x_in = A[self.blocks[bi - 1]["name"] + "output"] if bi > 0 else A["stem_activation"]
+            gx_in = G[self.blocks[bi - 1]["name"] + "output"] if bi > 0 else G["stem_activation"]
+            self._block_bwd(blk, x_in, gx_in)
+        rows = B * A["stem_pre"].shape[1] * A["stem_pre"].shape[2]
+        self.stem_bn.bwd(A["stem_pre"], G["stem_activation"], rows, "swish", None)
+
+    def _block_bwd(self, blk, x_in, gx_in):
+        A, G, B, n = self.act, self.gact, self.B, blk["name"]
+        h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
+        rows = B * oh * ow
+        gy = G[n + "output"]
+        if blk["residual"]:
+            drop = blk["drop"] if (self.drop_connect and blk["rate"] > 0) else None
+            if drop is not None:
+                K.scale_per_sample(gy, drop, blk["dbn"])
+                gbn = blk["dbn"]
+            else:
+                gbn = gy
+        else:
+            gbn = gy
+        gp = self._gpre_buf(A[n + "project_pre"].shape)
+        blk["project_bn"].bwd(A[n + "project_pre"], gbn, rows, "none", gp)
+        gse = G[n + "se_excite"]
+        K.conv2d_dgrad(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"]),
+                       gp, blk["project"].w_dg, gse)
+        F = self.frozen
+        K.se_bwd(gse, A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
+                 F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), blk["z1"], blk["gate"],
+                 blk["addn"])
+        gdw = self._gpre_buf(A[n + "dw_pre"].shape)
+        blk["bn"].bwd(A[n + "dw_pre"], gse, rows, "swish", gdw, gate=blk["gate"],
+                      addn=blk["addn"], hw=oh * ow)
+        pt, pl = blk["pad"]
+        if blk["ex"] != 1:
+            ge = G[n + "expand_activation"]
+            # skip taps already hold the decoder's gradient: accumulate onto it
+            is_tap = n + "expand_activation" in ("block6a_expand_activation",
+                                                 "block4a_expand_activation",
+                                                 "block3a_expand_activation")
+            K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
+            gpe = self._gpre_buf(A[n + "expand_pre"].shape)
+            blk["expand_bn"].bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
+            K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"]), gpe,
+                           blk["expand"].w_dg, gx_in)
+        else:
+            K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)
+        if blk["residual"]:
+            K.residual_add(gx_in, None, gy, gx_in)
+
+    # ------------------------------------------------------------------ optimizer
+    def adam_state(self):
+        if not hasattr(self, "_adam"):
+            self._adam = [torch.zeros_like(self.params.buf) for _ in range(3)]
+        return self._adam
+
+    def adam_step(self, lr, step, grad_scale=1.0, beta1=0.9, beta2=0.999, eps=1e-7):
+        m, v, vh = self.adam_state()
+        K.adam_amsgrad(self.params.buf, self.grads.buf, m, v, vh, lr, step, beta1, beta2, eps,
+                       grad_scale)
+        self.refresh_trainable()
+
+    # ------------------------------------------------------------------ counts
+    def count_trainable(self):
+        return sum(int(np.prod(s)) for _, s, _ in self.params.specs)
+
+    def conv_flops_per_image(self):
+        """Algorithmic dense-conv FLOPs per image of one train step (fwd + dX; dW for the
+        trainable decoder; no stem dX), the SURVEY §8d accounting."""
+        H, W = self.H, self.W
+        f = 0.0
+
+        def macs(h, w, k, cin, cout):
+            return h * w * k * k * cin * cout
+
+        h, w = H // 2, W // 2
+        f += macs(h, w, 3, 3, 32)  # stem fwd only
+        for blk in self.blocks:
+            if blk["ex"] != 1:
+                f += 2 * macs(blk["h"], blk["w"], 1, blk["cin"], blk["cexp"])
+            f += 2 * macs(blk["oh"], blk["ow"], 1, blk["cexp"], blk["cout"])
+        hh, ww = blk["oh"], blk["ow"]
+        f += 2 * macs(hh, ww, 1, 320, 1280)
+        cin = 1280
+        for conv, _, skip in self.dec:
+            f += 3 * macs(hh, ww, 3, conv.cin, conv.cout)
+            hh, ww = 2 * hh, 2 * ww
+        f += 3 * macs(hh, ww, 3, 32, 1)
+        return 2.0 * f
