@@ -1,0 +1,263 @@
+"""PLDepth training-step throughput on MI355X (BASELINE.json metric: images/s at 448x448,
+ranking_size=5, ff_effnet, per-GPU batch 32, Info sampler, Adam-AMSGrad; synthetic data).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A step = GPU ranking sampler + ff_effnet forward + ListMLE + backward + (RCCL all-reduce) +
+Adam-AMSGrad + filter refresh, on a resident synthetic batch, replayed from hipGraphs. Rank 0
+prints one JSON line. See DESIGN.md §Measurement for the roofline and cpu_baseline definitions.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+
+
+def synthetic_batch(B, H, W, seed):
+    """x ~ U[0,1); gt = smooth 8-bit-quantised depth field; mask ~ Bernoulli(0.9)."""
+    rng = np.random.default_rng(seed)
+    x = rng.random((B, H, W, 3), dtype=np.float32)
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    gt = np.empty((B, H, W), np.float32)
+    for b in range(B):
+        f = np.zeros((H, W))
+        for _ in range(6):
+            fy, fx = rng.uniform(0.3, 3.0, 2)
+            ph = rng.uniform(0, 2 * np.pi, 2)
+            f += rng.uniform(0.2, 1.0) * np.sin(2 * np.pi * fy * yy + ph[0]) * \
+                np.cos(2 * np.pi * fx * xx + ph[1])
+        f = (f - f.min()) / (f.max() - f.min())
+        gt[b] = np.round(255 * f).astype(np.float32) / np.float32(255)
+    mask = (rng.random((B, H, W)) < 0.9).astype(np.float32)
+    return x, gt, mask
+
+
+def profile_conv(trainer, lr):
+    """One eager step with HIP events around every implicit-GEMM conv launch (on the stream the
+    kernels run on). Returns (algorithmic FLOPs, seconds) of the conv_igemm family."""
+    from pldepth_amd import kernels as K
+    st = trainer.stream
+    recs = []
+    orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad")}
+
+    def flops_of(name, a):
+        C = a.c1 + a.c2
+        if name == "conv2d_dgrad":
+            return 2.0 * a.n * a.h * a.w * C * a.kh * a.kw * a.cout
+        return 2.0 * a.n * a.oh * a.ow * a.cout * a.kh * a.kw * C
+
+    def wrap(name):
+        fn = orig[name]
+
+        def w(args, *rest, **kw):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            r = fn(args, *rest, **kw)
+            e1.record(st)
+            recs.append((flops_of(name, args), e0, e1))
+            return r
+        return w
+
+    for n in orig:
+        setattr(K, n, wrap(n))
+    try:
+        trainer.step_eager(lr)
+        st.synchronize()
+    finally:
+        for n, f in orig.items():
+            setattr(K, n, f)
+    fl = sum(r[0] for r in recs)
+    sec = sum(r[1].elapsed_time(r[2]) for r in recs) / 1e3
+    return fl, sec, len(recs)
+
+
+def cpu_baseline(H, W, L, R, seconds_budget=25.0):
+    """The oracle (torch-CPU fp32 restatement of the full step + numpy sampler restatement),
+    8 threads as the reference's init_tensorflow(num_threads=8), on a bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import effnet as OE
+    from oracle import listmle as LM
+    from oracle import sampler as S
+    from pldepth_amd.models.effnet_ff import FlatStore  # noqa: F401  (names only)
+    torch.set_num_threads(8)
+    B = 2
+    x, gt, mask = synthetic_batch(B, H, W, seed=123)
+    w = _cpu_weights(H, W)
+    P = {k: torch.tensor(v) for k, v in w.items()}
+    names = sorted(OE.trainable_names(P))
+    from oracle.adam import adam_amsgrad_step
+    adam = {k: [np.zeros(P[k].shape, np.float32) for _ in range(3)] for k in names}
+    np.random.seed(0)
+
+    def one_step(step):
+        ys = [S.sample_masked_point_batch("info", mask[b], gt[b], R, L)[0] for b in range(B)]
+        y = np.stack(ys)
+        Q = {k: (v.clone().requires_grad_(True) if k in names else v) for k, v in P.items()}
+        out = OE.forward(Q, torch.tensor(x))
+        loss, dpred = LM.hourglass_nll(y, out.detach().numpy(), B, L)
+        out.backward(torch.tensor(dpred, dtype=torch.float32))
+        for k in names:  # Adam-AMSGrad (oracle/adam.py) on every trainable tensor
+            p, *st = adam_amsgrad_step(P[k].numpy(), Q[k].grad.numpy(), *adam[k], lr=1e-3,
+                                       step=step)
+            P[k] = torch.from_numpy(p)
+            adam[k] = st
+
+    one_step(1)  # warm-up
+    n_steps, t_total = 0, 0.0
+    while n_steps < 10 and t_total < seconds_budget:
+        t0 = time.perf_counter()
+        one_step(n_steps + 2)
+        t_total += time.perf_counter() - t0
+        n_steps += 1
+    return {"value": B * n_steps / t_total, "unit": "images/s", "cores": 8, "kind": "port",
+            "sample": f"{n_steps} timed full train steps after 1 warm-up (numpy Info sampler + "
+                      f"torch-CPU fp32 ff_effnet fwd/bwd + ListMLE + Adam-AMSGrad), batch {B}, "
+                      f"{H}x{W}, L={L}, R={R}, torch.set_num_threads(8)"}
+
+
+def _cpu_weights(H, W):
+    # the engine's initialiser, run on CPU buffers (no GPU needed)
+    from pldepth_amd.models import effnet_ff as E
+
+    class _CPU(E.EffNetFF):
+        def __init__(self):
+            self.H, self.W, self.B = H, W, 1
+            self.device = torch.device("cpu")
+            self.params, self.frozen, self.stats = E.FlatStore(), E.FlatStore(), E.FlatStore()
+            self.bns, self.convs = [], []
+            self._build_spec()
+            for s in (self.params, self.frozen, self.stats):
+                s.materialize("cpu")
+
+        def set_weights(self, w):
+            for store in (self.params, self.frozen, self.stats):
+                for name, shape, _ in store.specs:
+                    store[name].copy_(torch.as_tensor(np.asarray(w[name], np.float32)))
+
+    e = _CPU()
+    e.init_weights(0)
+    return e.get_weights()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=448)
+    ap.add_argument("--ranking-size", type=int, default=5)
+    ap.add_argument("--rankings-per-image", type=int, default=100)
+    ap.add_argument("--sampling-type", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world}"
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+        pg = dist.group.WORLD
+
+    from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
+    from pldepth_amd.trainer import ReplicaTrainer
+
+    H = W = a.size
+    B, L, R = a.batch, a.ranking_size, a.rankings_per_image
+    tr = ReplicaTrainer((H, W, 3), B, L, R, a.sampling_type, seed=0, rank=rank,
+                        world_size=world, process_group=pg)
+    x, gt, mask = synthetic_batch(B, H, W, seed=1000 + rank)
+    tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
+                 torch.from_numpy(mask).cuda())
+    lr = 0.01
+    # first step eager: sizes every workspace, then capture the graph(s)
+    tr.step_eager(lr)
+    torch.cuda.synchronize()
+    if not a.no_graph:
+        tr.capture()
+    for _ in range(max(a.warmup - 1, 0)):
+        tr.step(lr)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.step(lr)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = tr.loss_value()
+    value = world * B * a.steps / elapsed
+
+    # conv_igemm family: algorithmic FLOPs / measured duration (HIP events, eager step)
+    fl, sec, nlaunch = profile_conv(tr, lr)
+    achieved = fl / sec / 1e12
+    flops_img = tr.engine.conv_flops_per_image()
+    out = {
+        "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
+        "value": round(value, 3),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (U[0,1) RGB, smooth 8-bit depth, Bernoulli(0.9) mask; Keras-default "
+                "random-init weights)",
+        "config": {"workload": f"ff_effnet train step {H}x{W}, per-GPU batch {B}, "
+                               f"ranking_size {L}, rankings_per_image {R}, "
+                               f"sampler {tr.strategy}, Adam-AMSGrad",
+                   "model": "ff_effnet", "global_batch": world * B, "input": f"{H}x{W}",
+                   "ranking_size": L, "rankings_per_image": R,
+                   "parallelism": f"dp{world}", "graph": not a.no_graph},
+        "roofline": {
+            "bound": "mfma", "kernel": "conv_igemm_kernel (fwd/dgrad/wgrad, fp32 MFMA)",
+            "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "launches": nlaunch, "flops_per_step": fl,
+            "step_frac": round(value / world * flops_img / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+        },
+        "loss": loss,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(H, W, L, R)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

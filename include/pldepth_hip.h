@@ -66,6 +66,16 @@ int pld_adam_amsgrad(float* param, const float* grad, float* m, float* v, float*
                      float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,
                      void* stream);
 
+/* graph-replayable form: lr and the step counter are read from device memory at run time
+ * (lr_dev[0], step_dev[0] >= 1), so one captured hipGraph serves every step */
+int pld_adam_amsgrad_dev(float* param, const float* grad, float* m, float* v, float* vhat,
+                         int64_t n, const float* lr_dev, const int64_t* step_dev, float beta1,
+                         float beta2, float eps, float grad_scale, void* stream);
+/* step_dev[0] += 1 (the in-graph step counter) */
+int pld_step_increment(int64_t* step_dev, void* stream);
+/* dev[0] = value (stream-ordered; sets the per-step learning rate ahead of a graph replay) */
+int pld_set_scalar_f32(float* dev, float value, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Convolution (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32): replaces Keras Conv2D /
  * TF Conv2D + Conv2DBackpropInput + Conv2DBackpropFilter (pl_hourglass.py:59-96 decoder, the
@@ -167,6 +177,9 @@ int pld_residual_add(const float* a, const float* sample_scale, const float* b, 
  * image_offset+i, step). */
 int pld_dropconnect_scales(float* scales, int n, float rate, uint64_t seed, uint64_t step,
                            int layer, int image_offset, void* stream);
+int pld_dropconnect_scales_dev(float* scales, int n, float rate, uint64_t seed,
+                               const int64_t* step_dev, int layer, int image_offset,
+                               void* stream);
 /* y[i] = x[i] * sample_scale[img] (+ y[i] when accumulate) */
 int pld_scale_per_sample(const float* x, const float* sample_scale, int n, int64_t elems_per_img,
                          float* y, int accumulate, void* stream);
@@ -211,6 +224,9 @@ int pld_sampler_compact(const float* mask, int B, int H, int W, const float* gt,
                         int* nvalid, float* gt_minmax, void* ws, void* stream);
 int pld_sampler_draw(const int* nvalid, int B, int n_cand, int L, uint64_t seed, uint64_t step,
                      int image_offset, int* draws, void* stream);
+/* graph-replayable form: the Philox step counter is read from step_dev[0] */
+int pld_sampler_draw_dev(const int* nvalid, int B, int n_cand, int L, uint64_t seed,
+                         const int64_t* step_dev, int image_offset, int* draws, void* stream);
 int pld_sampler_rank(const float* gt, const int* valid_idx, const int* nvalid,
                      const float* gt_minmax, const int* draws, int B, int H, int W, int R, int L,
                      int strategy, float* out, void* ws, void* stream);

@@ -39,6 +39,11 @@ _SIGS = {
     "pld_version": (I32, []),
     "pld_listmle_fwd_bwd": (I32, [P, P, I32, I32, I32, I32, P, P, P, I32, P]),
     "pld_adam_amsgrad": (I32, [P, P, P, P, P, I64, F32, F32, F32, F32, I64, F32, P]),
+    "pld_adam_amsgrad_dev": (I32, [P, P, P, P, P, I64, P, P, F32, F32, F32, F32, P]),
+    "pld_step_increment": (I32, [P, P]),
+    "pld_set_scalar_f32": (I32, [P, F32, P]),
+    "pld_sampler_draw_dev": (I32, [P, I32, I32, I32, U64, P, I32, P, P]),
+    "pld_dropconnect_scales_dev": (I32, [P, I32, F32, U64, P, I32, I32, P]),
     "pld_conv2d_fwd": (I32, [C.POINTER(ConvArgs), P, P, P, I32, P]),
     "pld_conv2d_dgrad": (I32, [C.POINTER(ConvArgs), P, P, P, I32, P, I32, P]),
     "pld_conv2d_wgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),

@@ -149,9 +149,11 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
 }
 
 __global__ void dropconnect_kernel(float* __restrict__ sc, int n, float rate, uint64_t seed,
-                                   uint64_t step, int layer, int off) {
+                                   uint64_t step_arg, const int64_t* __restrict__ step_dev,
+                                   int layer, int off) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const uint64_t step = step_dev ? (uint64_t)step_dev[0] : step_arg;
   uint4 c = make_uint4((uint32_t)layer, (uint32_t)(off + i), (uint32_t)step,
                        (uint32_t)(step >> 32) ^ 0x5D0Cu);
   uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
@@ -210,7 +212,17 @@ extern "C" int pld_dropconnect_scales(float* scales, int n, float rate, uint64_t
                                       uint64_t step, int layer, int image_offset, void* stream) {
   PLD_CHECK_ARG(scales && n > 0 && rate >= 0.f && rate < 1.f, "pld_dropconnect_scales: bad args");
   dropconnect_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(scales, n, rate, seed, step,
-                                                                  layer, image_offset);
+                                                                  nullptr, layer, image_offset);
+  return check_launch("dropconnect_kernel");
+}
+
+extern "C" int pld_dropconnect_scales_dev(float* scales, int n, float rate, uint64_t seed,
+                                          const int64_t* step_dev, int layer, int image_offset,
+                                          void* stream) {
+  PLD_CHECK_ARG(scales && step_dev && n > 0 && rate >= 0.f && rate < 1.f,
+                "pld_dropconnect_scales_dev: bad args");
+  dropconnect_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(scales, n, rate, seed, 0,
+                                                                  step_dev, layer, image_offset);
   return check_launch("dropconnect_kernel");
 }
 

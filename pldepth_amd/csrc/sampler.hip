@@ -87,7 +87,9 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 }
 
 __global__ void draw_kernel(const int* __restrict__ nvalid, int B, int per_img, uint64_t seed,
-                            uint64_t step, int image_offset, int* __restrict__ draws) {
+                            uint64_t step_arg, const int64_t* __restrict__ step_dev,
+                            int image_offset, int* __restrict__ draws) {
+  const uint64_t step = step_dev ? (uint64_t)step_dev[0] : step_arg;
   const long total = (long)B * per_img;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long)gridDim.x * blockDim.x) {
@@ -302,7 +304,18 @@ extern "C" int pld_sampler_draw(const int* nvalid, int B, int n_cand, int L, uin
   PLD_CHECK_ARG(nvalid && draws && B > 0 && n_cand > 0 && L > 0, "pld_sampler_draw: bad args");
   const long total = (long)B * n_cand * L;
   draw_kernel<<<std::min<unsigned>(cdiv(total, 256), 4096), 256, 0, as_stream(stream)>>>(
-      nvalid, B, n_cand * L, seed, step, image_offset, draws);
+      nvalid, B, n_cand * L, seed, step, nullptr, image_offset, draws);
+  return check_launch("draw_kernel");
+}
+
+extern "C" int pld_sampler_draw_dev(const int* nvalid, int B, int n_cand, int L, uint64_t seed,
+                                    const int64_t* step_dev, int image_offset, int* draws,
+                                    void* stream) {
+  PLD_CHECK_ARG(nvalid && draws && step_dev && B > 0 && n_cand > 0 && L > 0,
+                "pld_sampler_draw_dev: bad args");
+  const long total = (long)B * n_cand * L;
+  draw_kernel<<<std::min<unsigned>(cdiv(total, 256), 4096), 256, 0, as_stream(stream)>>>(
+      nvalid, B, n_cand * L, seed, 0, step_dev, image_offset, draws);
   return check_launch("draw_kernel");
 }
 

@@ -61,6 +61,48 @@ def adam_amsgrad(param, grad, m, v, vhat, lr, step, beta1=0.9, beta2=0.999, eps=
                            float(lr), beta1, beta2, eps, int(step), float(grad_scale), stream())
 
 
+def adam_amsgrad_dev(param, grad, m, v, vhat, lr_dev, step_dev, beta1=0.9, beta2=0.999,
+                     eps=1e-7, grad_scale=1.0):
+    lib().pld_adam_amsgrad_dev(ptr(param), ptr(grad), ptr(m), ptr(v), ptr(vhat), param.numel(),
+                               ptr(lr_dev), ptr(step_dev), beta1, beta2, eps, float(grad_scale),
+                               stream())
+
+
+def step_increment(step_dev):
+    lib().pld_step_increment(ptr(step_dev), stream())
+
+
+def set_scalar(dev_tensor, value):
+    lib().pld_set_scalar_f32(ptr(dev_tensor), float(value), stream())
+
+
+class Graph:
+    """A hipGraph captured from the current stream (pld_graph_*)."""
+
+    def __init__(self):
+        self.exec = None
+
+    def capture(self, fn):
+        lib().pld_graph_begin(stream())
+        try:
+            fn()
+        finally:
+            h = C.c_void_p()
+            lib().pld_graph_end(stream(), C.byref(h))
+        self.exec = h
+        return self
+
+    def launch(self):
+        lib().pld_graph_launch(self.exec, stream())
+
+    def __del__(self):
+        if self.exec is not None:
+            try:
+                lib().pld_graph_destroy(self.exec)
+            except Exception:
+                pass
+
+
 # ------------------------------------------------------------------------------------ conv
 def same_pads(h, k, s):
     """TF 'same' padding: (pad_before, out)."""
@@ -172,8 +214,13 @@ def residual_add(a, sample_scale, b, y):
 
 
 def dropconnect_scales(scales, rate, seed, step, layer, image_offset=0):
-    lib().pld_dropconnect_scales(ptr(scales), scales.numel(), float(rate), seed, step, layer,
-                                 image_offset, stream())
+    """step: an int, or a device int64 tensor (graph-replayable counter)."""
+    if isinstance(step, torch.Tensor):
+        lib().pld_dropconnect_scales_dev(ptr(scales), scales.numel(), float(rate), seed,
+                                         ptr(step), layer, image_offset, stream())
+    else:
+        lib().pld_dropconnect_scales(ptr(scales), scales.numel(), float(rate), seed, step, layer,
+                                     image_offset, stream())
 
 
 def bn_inference_coeffs(gamma, beta, mmean, mvar, scale, shift, eps=1e-3):
@@ -230,9 +277,14 @@ def sampler_compact(mask, gt, valid_idx, nvalid, gt_minmax):
 
 
 def sampler_draw(nvalid, n_cand, L, seed, step, image_offset, draws):
+    """step: an int, or a device int64 tensor (graph-replayable counter)."""
     B = nvalid.shape[0]
-    lib().pld_sampler_draw(ptr(nvalid), B, n_cand, L, seed, step, image_offset, ptr(draws),
-                           stream())
+    if isinstance(step, torch.Tensor):
+        lib().pld_sampler_draw_dev(ptr(nvalid), B, n_cand, L, seed, ptr(step), image_offset,
+                                   ptr(draws), stream())
+    else:
+        lib().pld_sampler_draw(ptr(nvalid), B, n_cand, L, seed, step, image_offset, ptr(draws),
+                               stream())
 
 
 def sampler_rank(gt, valid_idx, nvalid, gt_minmax, draws, R, L, strategy, out):

@@ -377,7 +377,10 @@ class EffNetFF:
         return self._gpre[key]
 
     # ------------------------------------------------------------------ forward
-    def forward(self, training=True, step=0):
+    def forward(self, training=True, step=0, image_offset=0):
+        """step: int or device int64 tensor (drop-connect Philox counter); image_offset: global
+        index of this replica's first image (draws independent of the GPU count)."""
+        self._img_off = image_offset
         A = self.act
         B = self.B
         a = K.conv_args
@@ -453,7 +456,8 @@ class EffNetFF:
         if blk["residual"]:
             drop = None
             if training and self.drop_connect and blk["rate"] > 0:
-                K.dropconnect_scales(blk["drop"], blk["rate"], self.seed, step, li)
+                K.dropconnect_scales(blk["drop"], blk["rate"], self.seed, step, li,
+                                     getattr(self, "_img_off", 0))
                 drop = blk["drop"]
             K.residual_add(out, drop, x, out)
         return out

@@ -1,0 +1,136 @@
+"""One data-parallel replica of the PLDepth training step, end to end on the GPU.
+
+Replaces, per step, what ``model.fit`` (pldepth/PLDepth.py:176) drives: the ranking sampler the
+reference runs on the host under tf.numpy_function (hourglass_provider.py:55-58 ->
+sampling.py), the ff_effnet forward/backward (pl_hourglass.py:45-100), the ListMLE loss
+(nll_loss.py:32-62) and Adam(amsgrad) (PLDepth.py:133) — plus, for N > 1 GPUs, the gradient
+all-reduce the reference never had: one process per GPU, torch.distributed with the
+"nccl" backend (= RCCL over xGMI), per-rank batch B, BN statistics per replica (MirroredStrategy
+semantics), one fp32 all-reduce of the flat gradient buffer, 1/world folded into Adam.
+
+Graph structure: the whole step is stream-ordered HIP work with no host synchronisation, captured
+once into hipGraphs (N = 1: one graph; N > 1: [sampler + fwd + bwd] -> all-reduce -> [Adam +
+filter refresh + step++]). Per-step scalars (learning rate, step counter) live in device memory.
+"""
+import numpy as np
+import torch
+
+from . import kernels as K
+from .models.effnet_ff import EffNetFF
+
+SAMPLING_TYPES = {0: "thresh", 1: "info", 3: "pure"}  # PLDepth.py:97-108 --sampling_type
+
+
+class ReplicaTrainer:
+    def __init__(self, input_shape=(448, 448, 3), batch_size=32, ranking_size=5,
+                 rankings_per_image=100, sampling_type=1, seed=0, rank=0, world_size=1,
+                 process_group=None, model="ff_effnet", drop_connect=True):
+        if model != "ff_effnet":
+            raise NotImplementedError(f"model {model!r}: only ff_effnet has a HIP engine yet")
+        self.B, self.L, self.R = batch_size, ranking_size, rankings_per_image
+        self.H, self.W = input_shape[:2]
+        self.strategy = SAMPLING_TYPES[sampling_type] if isinstance(sampling_type, int) \
+            else sampling_type
+        self.rank, self.world = rank, world_size
+        self.pg = process_group
+        self.seed = seed
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.engine = EffNetFF(input_shape, batch_size, device=dev, seed=seed)
+        self.engine.drop_connect = drop_connect
+        B, H, W, L, R = self.B, self.H, self.W, self.L, self.R
+        self.n_cand = K.sampler_candidates(R, self.strategy)
+        self.R_out = self.n_cand if self.strategy == "pure" else R
+        # data (resident in HBM): image batch lives in the engine's input buffer
+        self.x = self.engine.act["input"]
+        self.gt = torch.zeros(B, H, W, device=dev)
+        self.mask = torch.ones(B, H, W, device=dev)
+        # sampler state
+        self.valid_idx = torch.empty(B, H * W, dtype=torch.int32, device=dev)
+        self.nvalid = torch.empty(B, dtype=torch.int32, device=dev)
+        self.minmax = torch.empty(B, 2, device=dev)
+        self.draws = torch.empty(B, self.n_cand, L, dtype=torch.int32, device=dev)
+        self.y_true = torch.empty(B, self.R_out, L, 2, device=dev)
+        # loss state
+        self.nll = torch.empty(B * self.R_out, device=dev)
+        self.loss = torch.zeros(1, device=dev)
+        self.dpred = torch.empty(B, H, W, 1, device=dev)
+        # per-step scalars on the device
+        self.step_dev = torch.ones(1, dtype=torch.int64, device=dev)
+        self.lr_dev = torch.full((1,), 0.01, device=dev)
+        self.m, self.v, self.vhat = self.engine.adam_state()
+        self.graphs = None
+        self.stream = torch.cuda.Stream(device=dev)
+
+    # ------------------------------------------------------------------ data
+    def set_batch(self, images, gt, mask):
+        """images [B,H,W,3] in [0,1], gt [B,H,W], mask [B,H,W] (>0 valid) — host or device."""
+        self.x.copy_(torch.as_tensor(images, dtype=torch.float32))
+        self.gt.copy_(torch.as_tensor(gt, dtype=torch.float32))
+        self.mask.copy_(torch.as_tensor(mask, dtype=torch.float32))
+
+    # ------------------------------------------------------------------ phases
+    def _sample(self):
+        K.sampler_compact(self.mask, self.gt, self.valid_idx, self.nvalid, self.minmax)
+        K.sampler_draw(self.nvalid, self.n_cand, self.L, self.seed, self.step_dev,
+                       self.rank * self.B, self.draws)
+        K.sampler_rank(self.gt, self.valid_idx, self.nvalid, self.minmax, self.draws, self.R,
+                       self.L, self.strategy, self.y_true)
+
+    def _fwd_bwd(self):
+        eng = self.engine
+        eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
+        K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
+                          dpred=self.dpred, nll=self.nll, loss=self.loss, zero_dpred=True)
+        eng.backward(self.dpred)
+
+    def _update(self):
+        eng = self.engine
+        K.adam_amsgrad_dev(eng.params.buf, eng.grads.buf, self.m, self.v, self.vhat, self.lr_dev,
+                           self.step_dev, grad_scale=1.0 / self.world)
+        eng.refresh_trainable()
+        K.step_increment(self.step_dev)
+
+    def _allreduce(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.engine.grads.buf, group=self.pg)
+
+    # ------------------------------------------------------------------ driving
+    def step_eager(self, lr):
+        with torch.cuda.stream(self.stream):
+            K.set_scalar(self.lr_dev, lr)
+            self._sample()
+            self._fwd_bwd()
+            self._allreduce()
+            self._update()
+
+    def capture(self):
+        """Capture the step into hipGraph(s). Call after one eager step (workspaces sized)."""
+        torch.cuda.synchronize()
+        with torch.cuda.stream(self.stream):
+            if self.world == 1:
+                g = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd(), self._update()))
+                self.graphs = [g]
+            else:
+                ga = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd()))
+                gb = K.Graph().capture(self._update)
+                self.graphs = [ga, gb]
+        torch.cuda.synchronize()
+
+    def step(self, lr):
+        if self.graphs is None:
+            return self.step_eager(lr)
+        with torch.cuda.stream(self.stream):
+            K.set_scalar(self.lr_dev, lr)
+            self.graphs[0].launch()
+            if self.world > 1:
+                self._allreduce()
+                self.graphs[1].launch()
+
+    def loss_value(self):
+        torch.cuda.current_stream().wait_stream(self.stream)
+        return float(self.loss.item())
+
+    def synchronize(self):
+        self.stream.synchronize()
