@@ -153,18 +153,38 @@ static int launch_reduce(int op, RedParams& p, hipStream_t st) {
   return check_launch("chan_reduce_kernel");
 }
 
-// ---- finalize kernels: sum the nbx partials of each channel in order ----
-__global__ void stats_finalize_kernel(const double* __restrict__ part, int nbx, int C, long rows,
-                                      float eps, float momentum, float* __restrict__ mean,
-                                      float* __restrict__ invstd, float* __restrict__ mmean,
-                                      float* __restrict__ mvar) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nbx; ++b) {
-    s += part[((long)b * C + c) * 2];
-    q += part[((long)b * C + c) * 2 + 1];
+// ---- finalize kernels: one workgroup per channel sums that channel's nbx partials (strided
+// over the 256 threads, then a fixed-shape tree: deterministic, latency-parallel) ----
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ part, int nbx, int C,
+                                                int c, double& s, double& q) {
+  __shared__ double rs[256], rq[256];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < nbx; i += 256) {
+    a += part[((long)i * C + c) * 2];
+    b += part[((long)i * C + c) * 2 + 1];
   }
+  rs[threadIdx.x] = a;
+  rq[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rq[threadIdx.x] += rq[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  s = rs[0];
+  q = rq[0];
+}
+
+__global__ __launch_bounds__(256) void stats_finalize_kernel(
+    const double* __restrict__ part, int nbx, int C, long rows, float eps, float momentum,
+    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ mmean,
+    float* __restrict__ mvar) {
+  const int c = blockIdx.x;
+  double s, q;
+  reduce_partials(part, nbx, C, c, s, q);
+  if (threadIdx.x != 0) return;
   const double n = (double)rows;
   const double mu = s / n;
   double var = q / n - mu * mu;
@@ -179,26 +199,23 @@ __global__ void stats_finalize_kernel(const double* __restrict__ part, int nbx, 
   }
 }
 
-__global__ void sum_finalize_kernel(const double* __restrict__ part, int nbx, int C,
-                                    float* __restrict__ out, int acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int b = 0; b < nbx; ++b) s += part[((long)b * C + c) * 2];
-  out[c] = acc ? out[c] + (float)s : (float)s;
+__global__ __launch_bounds__(256) void sum_finalize_kernel(const double* __restrict__ part,
+                                                           int nbx, int C,
+                                                           float* __restrict__ out, int acc) {
+  const int c = blockIdx.x;
+  double s, q;
+  reduce_partials(part, nbx, C, c, s, q);
+  if (threadIdx.x == 0) out[c] = acc ? out[c] + (float)s : (float)s;
 }
 
 // writes dgamma/dbeta and the per-channel coefficients k1 = mean(dz), k2 = mean(dz*xhat)
-__global__ void bnbwd_finalize_kernel(const double* __restrict__ part, int nbx, int C, long rows,
-                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                      int pacc, float* __restrict__ k12) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nbx; ++b) {
-    s += part[((long)b * C + c) * 2];
-    q += part[((long)b * C + c) * 2 + 1];
-  }
+__global__ __launch_bounds__(256) void bnbwd_finalize_kernel(
+    const double* __restrict__ part, int nbx, int C, long rows, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int pacc, float* __restrict__ k12) {
+  const int c = blockIdx.x;
+  double s, q;
+  reduce_partials(part, nbx, C, c, s, q);
+  if (threadIdx.x != 0) return;
   if (dbeta) dbeta[c] = pacc ? dbeta[c] + (float)s : (float)s;
   if (dgamma) dgamma[c] = pacc ? dgamma[c] + (float)q : (float)q;
   k12[c] = (float)(s / (double)rows);
@@ -380,7 +397,7 @@ extern "C" int pld_channel_sum(const float* x, int64_t rows, int c, float* out, 
   if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
-  sum_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, out, accumulate);
+  sum_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, out, accumulate);
   return check_launch("sum_finalize_kernel");
 }
 
@@ -401,7 +418,7 @@ extern "C" int pld_bn_stats(const float* x, int64_t rows, int c, float eps, floa
   if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
-  stats_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, rows, eps, momentum,
+  stats_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, eps, momentum,
                                                        mean, invstd, moving_mean, moving_var);
   return check_launch("stats_finalize_kernel");
 }
@@ -487,7 +504,7 @@ extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, 
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
   float* k12 = reinterpret_cast<float*>((char*)ws + red_ws_doubles(rows, c) * sizeof(double));
-  bnbwd_finalize_kernel<<<cdiv(c, 256), 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
+  bnbwd_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
                                                        param_accumulate, k12);
   rc = check_launch("bnbwd_finalize_kernel");
   if (rc || !dx) return rc;

@@ -85,7 +85,7 @@ __device__ __forceinline__ float4 load_x4(const GemmConvParams& p, int img, int 
   return *reinterpret_cast<const float4*>(p.x2 + pix * p.c2 + (ci - p.c1));
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, bool VEC>
+template <int BM, int BN, int WM, int WN, int MODE, bool VEC, bool VEC16>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -155,6 +155,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
+    int s_ty = 0, s_tx = 0, s_ci = 0;
+    if (MODE == MODE_FWD && VEC16) {
+      const int tap = (int)p.dC.div((uint32_t)k0);
+      s_ci = k0 - tap * p.C;
+      s_ty = (int)p.dKW.div((uint32_t)tap);
+      s_tx = tap - s_ty * p.kw;
+    }
     if (MODE == MODE_FWD) {
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
@@ -163,7 +170,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
         const int k = k0 + 4 * kq;
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         if (a_ok[j]) {
-          if (VEC) {
+          if (VEC16) {
+            // C % 16 == 0 and c1 % 16 == 0: the whole 16-wide K-step sits in one tap and one
+            // source; its decomposition is wave-uniform (computed once above)
+            if (k0 < p.K)
+              val = load_x4(p, a_img[j], a_iy0[j] + s_ty, a_ix0[j] + s_tx, s_ci + 4 * kq);
+          } else if (VEC) {
             if (k < p.K) {
               const uint32_t tap = p.dC.div((uint32_t)k);
               const int ci = k - (int)tap * p.C;
@@ -436,21 +448,55 @@ __global__ void filter_dgrad_kernel(const float* __restrict__ w, int kh, int kw,
 }
 
 // ------------------------------------------------------------------------ dispatch
+// ---- tile configurations and a small cost model ----
+// (BM, BN, WM, WN): 4 waves; each wave computes (BM/WM) x (BN/WN) as 32x32 MFMA tiles.
+struct TileCfg { int bm, bn, tm, tn; };
+static const TileCfg kTiles[] = {
+    {256, 32, 2, 1},  {128, 64, 1, 1},  {128, 96, 1, 3},  {128, 128, 2, 2},
+    {128, 160, 1, 5}, {128, 192, 1, 6}, {128, 224, 1, 7},
+};
+
+// estimated relative time: padded MFMA work per block x waves of blocks over 256 CUs,
+// discounted by the per-wave tile count (fragment reuse)
+static int choose_tile(long M, long N, long K, int splits) {
+  int best = 0;
+  double best_t = 1e300;
+  for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
+    const TileCfg& t = kTiles[i];
+    const long blocks = (long)cdiv(M, t.bm) * cdiv(N, t.bn) * splits;
+    const int per_wave = t.tm * t.tn;
+    const double eff = per_wave >= 4 ? 1.0 : (per_wave == 3 ? 0.9 : (per_wave == 2 ? 0.8 : 0.55));
+    const int occ = (t.bn >= 160) ? 2 : 3;  // resident blocks per CU (VGPR bound)
+    const double rounds = std::ceil((double)blocks / (256.0 * occ));
+    const double t_est = rounds * occ * (double)t.bm * t.bn * ((double)K / splits) / eff;
+    if (t_est < best_t * 0.97) {
+      best_t = t_est;
+      best = i;
+    }
+  }
+  return best;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_cfg(GemmConvParams& p, bool vec, bool vec16, int splits, hipStream_t st) {
+  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
+  if (vec16) conv_igemm_kernel<BM, BN, WM, WN, MODE, true, true><<<grid, 256, 0, st>>>(p);
+  else if (vec) conv_igemm_kernel<BM, BN, WM, WN, MODE, true, false><<<grid, 256, 0, st>>>(p);
+  else conv_igemm_kernel<BM, BN, WM, WN, MODE, false, false><<<grid, 256, 0, st>>>(p);
+}
+
 template <int MODE>
-static int launch_igemm(GemmConvParams& p, bool vec, int splits, hipStream_t st) {
-  // tile selection by the GEMM's N (columns): skinny N uses 256x32 tiles
-  if (p.N <= 32) {
-    dim3 grid(cdiv(p.M, 256), cdiv(p.N, 32), splits);
-    if (vec) conv_igemm_kernel<256, 32, 4, 1, MODE, true><<<grid, 256, 0, st>>>(p);
-    else conv_igemm_kernel<256, 32, 4, 1, MODE, false><<<grid, 256, 0, st>>>(p);
-  } else if (p.N <= 64) {
-    dim3 grid(cdiv(p.M, 128), cdiv(p.N, 64), splits);
-    if (vec) conv_igemm_kernel<128, 64, 2, 2, MODE, true><<<grid, 256, 0, st>>>(p);
-    else conv_igemm_kernel<128, 64, 2, 2, MODE, false><<<grid, 256, 0, st>>>(p);
-  } else {
-    dim3 grid(cdiv(p.M, 128), cdiv(p.N, 128), splits);
-    if (vec) conv_igemm_kernel<128, 128, 2, 2, MODE, true><<<grid, 256, 0, st>>>(p);
-    else conv_igemm_kernel<128, 128, 2, 2, MODE, false><<<grid, 256, 0, st>>>(p);
+static int launch_igemm(GemmConvParams& p, bool vec, bool vec16, int splits, int cfg,
+                        hipStream_t st) {
+  if (MODE == MODE_WGRAD) vec16 = false;
+  switch (cfg) {
+    case 0: launch_cfg<MODE, 256, 32, 4, 1>(p, vec, vec16, splits, st); break;
+    case 1: launch_cfg<MODE, 128, 64, 2, 2>(p, vec, vec16, splits, st); break;
+    case 2: launch_cfg<MODE, 128, 96, 4, 1>(p, vec, vec16, splits, st); break;
+    case 3: launch_cfg<MODE, 128, 128, 2, 2>(p, vec, vec16, splits, st); break;
+    case 4: launch_cfg<MODE, 128, 160, 4, 1>(p, vec, vec16, splits, st); break;
+    case 5: launch_cfg<MODE, 128, 192, 4, 1>(p, vec, vec16, splits, st); break;
+    default: launch_cfg<MODE, 128, 224, 4, 1>(p, vec, vec16, splits, st); break;
   }
   return check_launch("conv_igemm_kernel");
 }
@@ -489,6 +535,16 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace pld;
 
+// direct kernels for the single-output-channel 3x3 conv (skinny.hip)
+extern "C" int pld__skinny_eligible(const pld_conv_args* a);
+extern "C" int pld__skinny_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,
+                               float* y, int accumulate, void* stream);
+extern "C" int pld__skinny_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
+                                 float* dx, int accumulate, void* stream);
+extern "C" size_t pld__skinny_wgrad_ws(const pld_conv_args* a);
+extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float* dw,
+                                 int accumulate, void* ws, void* stream);
+
 extern "C" int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout,
                                     float* w_ohwi, void* stream) {
   PLD_CHECK_ARG(w_hwio && w_ohwi && kh > 0 && kw > 0 && cin > 0 && cout > 0,
@@ -515,6 +571,8 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   int rc = fill_geom(a, p);
   if (rc) return rc;
   PLD_CHECK_ARG(w_ohwi && y, "pld_conv2d_fwd: null w/y");
+  if (pld__skinny_eligible(a) && aligned16(a->x1))
+    return pld__skinny_fwd(a, w_ohwi, bias, y, accumulate, stream);
   p.bmat = w_ohwi;
   p.M = a->n * a->oh * a->ow;
   p.N = a->cout;
@@ -527,7 +585,9 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   const bool vec = (p.c1 % 4 == 0) && (p.c2 % 4 == 0) && aligned16(p.x1) &&
                    (!p.x2 || aligned16(p.x2)) && aligned16(w_ohwi) &&
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
-  return launch_igemm<MODE_FWD>(p, vec, 1, as_stream(stream));
+  const bool vec16 = vec && (p.c1 % 16 == 0) && (p.c2 % 16 == 0);
+  return launch_igemm<MODE_FWD>(p, vec, vec16, 1, choose_tile(p.M, p.N, p.K, 1),
+                                as_stream(stream));
 }
 
 extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
@@ -538,6 +598,8 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   PLD_CHECK_ARG(a->c2 == 0 || dx2, "pld_conv2d_dgrad: dx2 required for a two-source conv");
   PLD_CHECK_ARG(a->in_scale == nullptr,
                 "pld_conv2d_dgrad: the input prologue's gradient is the caller's (pass NULL)");
+  if (pld__skinny_eligible(a) && aligned16(dx1))
+    return pld__skinny_dgrad(a, dy, w_dgrad, dx1, accumulate1, stream);
   // dx[img][iy][ix][ci] = sum_{ty,tx,co} dy[img][iy+ty-pt'][ix+tx-pl'][co] * Wd[ci][ty][tx][co]
   // with pt' = kh-1-pt and the output spatial = the forward input spatial.
   pld_conv_args g = *a;
@@ -569,19 +631,22 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   p.acc2 = accumulate2;
   p.split = a->c1;
   const bool vec = (p.c1 % 4 == 0) && aligned16(dy) && aligned16(w_dgrad);
-  return launch_igemm<MODE_FWD>(p, vec, 1, as_stream(stream));
+  const bool vec16 = vec && (p.c1 % 16 == 0);
+  return launch_igemm<MODE_FWD>(p, vec, vec16, 1, choose_tile(p.M, p.N, p.K, 1),
+                                as_stream(stream));
 }
 
 static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& splits,
-                       int& kt_per) {
+                       int& kt_per, int& cfg) {
   M = a->kh * a->kw * (a->c1 + a->c2);
   N = a->cout;
   K = (long)a->n * a->oh * a->ow;
-  const int bm = (N <= 32) ? 256 : 128, bn = (N <= 32) ? 32 : (N <= 64 ? 64 : 128);
-  const long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
   const long ktiles = (K + BK - 1) / BK;
-  long s = std::max<long>(1, (1024 + tiles - 1) / tiles);  // aim for ~1024 blocks
-  s = std::min<long>(s, std::max<long>(1, ktiles / 8));    // >= 8 k-steps per block
+  // pick the tile for an unsplit GEMM, then split K until ~3 blocks per CU
+  cfg = choose_tile(M, N, K, 1);
+  const long tiles = (long)cdiv(M, kTiles[cfg].bm) * cdiv(N, kTiles[cfg].bn);
+  long s = std::max<long>(1, (768 + tiles - 1) / tiles);
+  s = std::min<long>(s, std::max<long>(1, ktiles / 8));  // >= 8 k-steps per block
   kt_per = (int)((ktiles + s - 1) / s);
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
@@ -590,9 +655,10 @@ extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->kh <= 0 || a->kw <= 0 || a->c1 <= 0 || a->c2 < 0 || a->cout <= 0 ||
       a->oh <= 0 || a->ow <= 0)
     return 0;
-  int M, N, splits, kt;
+  if (pld__skinny_eligible(a)) return pld__skinny_wgrad_ws(a);
+  int M, N, splits, kt, cfg;
   long K;
-  wgrad_plan(a, M, N, K, splits, kt);
+  wgrad_plan(a, M, N, K, splits, kt, cfg);
   return splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
 }
 
@@ -602,9 +668,15 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   int rc = fill_geom(a, p);
   if (rc) return rc;
   PLD_CHECK_ARG(dy && dw, "pld_conv2d_wgrad: null dy/dw");
-  int M, N, splits, kt_per;
+  if (pld__skinny_eligible(a) && aligned16(a->x1)) {
+    const size_t need = pld__skinny_wgrad_ws(a);
+    PLD_CHECK_ARG(ws && ws_bytes >= need, "pld_conv2d_wgrad: workspace %zu < %zu bytes",
+                  ws_bytes, need);
+    return pld__skinny_wgrad(a, dy, dw, accumulate, ws, stream);
+  }
+  int M, N, splits, kt_per, cfg;
   long K;
-  wgrad_plan(a, M, N, K, splits, kt_per);
+  wgrad_plan(a, M, N, K, splits, kt_per, cfg);
   PLD_CHECK_ARG(K < (1L << 31), "pld_conv2d_wgrad: too many pixels");
   const size_t need = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
   PLD_CHECK_ARG(ws_bytes >= need && (need == 0 || ws),
@@ -631,7 +703,7 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   const bool vec = (p.c1 % 4 == 0) && (p.c2 % 4 == 0) && aligned16(p.x1) &&
                    (!p.x2 || aligned16(p.x2)) && aligned16(dy) &&
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
-  rc = launch_igemm<MODE_WGRAD>(p, vec, splits, st);
+  rc = launch_igemm<MODE_WGRAD>(p, vec, false, splits, cfg, st);
   if (rc || splits == 1) return rc;
   const long n = (long)M * N;
   splitk_reduce_kernel<<<std::min<unsigned>(cdiv(n, 256), 4096), 256, 0, st>>>(

@@ -1,0 +1,243 @@
+// 3x3 'same' convolutions with ONE output channel (the decoder's final Conv2D(1, 3x3),
+// pldepth/models/pl_hourglass.py:96) as direct, LDS-tiled, HBM-bound kernels.
+//
+// An implicit GEMM with N = 1 wastes 31/32 of every 32x32 MFMA tile; the layer's arithmetic
+// (288 MACs per output pixel) is far below the HBM roofline, so each kernel instead streams its
+// big operand once: a 16x16 output tile stages its 18x18 input halo (all channels, chunked by 32)
+// in LDS, padded to a 36-float channel stride so 16 consecutive pixels' float4 reads hit 16
+// distinct LDS slots.
+//   fwd   : y[n][oy][ox] = b + sum_{ty,tx,c} x[n][oy+ty-pt][ox+tx-pl][c] * w[ty][tx][c]
+//   dgrad : dx[n][iy][ix][c] = sum_{ty,tx} dy[n][iy-ty+pt][ix-tx+pl] * w[ty][tx][c]
+//   wgrad : dw[ty][tx][c] = sum_{n,oy,ox} x[n][oy+ty-pt][ox+tx-pl][c] * dy[n][oy][ox]
+//           (per-workgroup partials over a strided set of tiles, ordered reduction)
+// Algorithmic bytes: fwd/wgrad read x once (+ dy), dgrad writes dx once.
+#include <algorithm>
+
+#include "common.h"
+
+namespace pld {
+
+constexpr int ST = 16;        // output tile edge
+constexpr int HT = ST + 2;    // halo edge (3x3)
+constexpr int CH = 32;        // channels per LDS chunk
+constexpr int CS = CH + 4;    // padded channel stride
+
+struct SkinnyParams {
+  const float* x;   // [n][h][w][c]
+  const float* dy;  // [n][h][w]
+  const float* wt;  // fwd: [3][3][c] (tap-major, = HWIO with cout 1); dgrad: [c][3][3] flipped
+  const float* bias;
+  float* y;         // fwd: [n][h][w]; dgrad: [n][h][w][c]
+  float* part;      // wgrad partials [gridDim.x][9*c]
+  int n, h, w, c, pt, pl, acc;
+  int tiles_x, tiles_y;
+};
+
+__device__ __forceinline__ void stage_halo(const SkinnyParams& p, float* halo, int img, int y0,
+                                           int x0, int c0, int nc) {
+  // halo[(hy*HT + hx)*CS + cc] = x[img][y0+hy-pt][x0+hx-pl][c0+cc], zero outside
+  const int nq = nc / 4;
+  for (int e = threadIdx.x; e < HT * HT * nq; e += blockDim.x) {
+    const int q = e % nq;
+    const int pix = e / nq;
+    const int hy = pix / HT, hx = pix % HT;
+    const int iy = y0 + hy - p.pt, ix = x0 + hx - p.pl;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (iy >= 0 && iy < p.h && ix >= 0 && ix < p.w)
+      v = *reinterpret_cast<const float4*>(p.x + (((long)img * p.h + iy) * p.w + ix) * p.c + c0 +
+                                           4 * q);
+    *reinterpret_cast<float4*>(halo + pix * CS + 4 * q) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void skinny_fwd_kernel(SkinnyParams p) {
+  __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
+  __shared__ __attribute__((aligned(16))) float wl[9 * CH];
+  const int tx = threadIdx.x % ST, ty = threadIdx.x / ST;
+  const int x0 = blockIdx.x * ST, y0 = blockIdx.y * ST, img = blockIdx.z;
+  float acc = 0.f;
+  for (int c0 = 0; c0 < p.c; c0 += CH) {
+    const int nc = min(CH, p.c - c0);
+    __syncthreads();
+    stage_halo(p, halo, img, y0, x0, c0, nc);
+    for (int e = threadIdx.x; e < 9 * nc; e += blockDim.x)
+      wl[(e / nc) * CH + e % nc] = p.wt[(e / nc) * p.c + c0 + e % nc];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float* hp = halo + ((ty + t / 3) * HT + tx + t % 3) * CS;
+      const float* wp = wl + t * CH;
+      for (int q = 0; q < nc; q += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(hp + q);
+        const float4 f = *reinterpret_cast<const float4*>(wp + q);
+        acc += v.x * f.x + v.y * f.y + v.z * f.z + v.w * f.w;
+      }
+    }
+  }
+  const int oy = y0 + ty, ox = x0 + tx;
+  if (oy < p.h && ox < p.w) {
+    float* d = p.y + ((long)img * p.h + oy) * p.w + ox;
+    const float v = acc + (p.bias ? p.bias[0] : 0.f);
+    *d = p.acc ? *d + v : v;
+  }
+}
+
+__global__ __launch_bounds__(256) void skinny_dgrad_kernel(SkinnyParams p) {
+  __shared__ float dyl[HT * HT];
+  __shared__ __attribute__((aligned(16))) float wl[9 * 64];
+  const int tx = threadIdx.x % ST, ty = threadIdx.x / ST;
+  const int x0 = blockIdx.x * ST, y0 = blockIdx.y * ST, img = blockIdx.z;
+  // dy halo: dyl[hy][hx] = dy[img][y0+hy-(2-pt)][x0+hx-(2-pl)]
+  const int qt = 2 - p.pt, ql = 2 - p.pl;
+  for (int e = threadIdx.x; e < HT * HT; e += blockDim.x) {
+    const int iy = y0 + e / HT - qt, ix = x0 + e % HT - ql;
+    dyl[e] = (iy >= 0 && iy < p.h && ix >= 0 && ix < p.w)
+                 ? p.dy[((long)img * p.h + iy) * p.w + ix] : 0.f;
+  }
+  const int iy = y0 + ty, ix = x0 + tx;
+  for (int c0 = 0; c0 < p.c; c0 += 64) {
+    const int nc = min(64, p.c - c0);
+    __syncthreads();
+    // p.w is the dgrad-native filter [c][3][3] with flipped taps: W[t][c] = Wd[c][8 - t]
+    for (int e = threadIdx.x; e < 9 * nc; e += blockDim.x)
+      wl[(e / nc) * 64 + e % nc] = p.wt[(long)(c0 + e % nc) * 9 + (8 - e / nc)];
+    __syncthreads();
+    if (iy < p.h && ix < p.w) {
+      float* d = p.y + (((long)img * p.h + iy) * p.w + ix) * p.c + c0;
+      for (int q = 0; q < nc; q += 4) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          // output (iy - ty + pt) contributes through tap ty: halo row iy-ty+pt-(y0-qt)
+          const int hy = ty + 2 - t / 3, hx = tx + 2 - t % 3;
+          const float g = dyl[hy * HT + hx];
+          const float4 f = *reinterpret_cast<const float4*>(wl + t * 64 + q);
+          a.x += g * f.x; a.y += g * f.y; a.z += g * f.z; a.w += g * f.w;
+        }
+        float4* dp = reinterpret_cast<float4*>(d + q);
+        if (p.acc) {
+          const float4 o = *dp;
+          a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+        }
+        *dp = a;
+      }
+    }
+  }
+}
+
+// 576 threads = 2 pixel halves x 288 (tap, channel) pairs: every thread does equal work
+constexpr int WG_THREADS = 576;
+
+__global__ __launch_bounds__(WG_THREADS) void skinny_wgrad_kernel(SkinnyParams p) {
+  __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
+  __shared__ float dyl[ST * ST];
+  __shared__ float comb[9 * CH];
+  const int ntiles = p.tiles_x * p.tiles_y * p.n;
+  const int nE = 9 * p.c;  // c <= CH (eligibility)
+  const int half = threadIdx.x / (9 * CH);
+  const int e = threadIdx.x % (9 * CH);
+  const int t = e / p.c, cc = e % p.c;
+  const bool act = e < nE;
+  float acc = 0.f;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int img = tile / (p.tiles_x * p.tiles_y);
+    const int r = tile % (p.tiles_x * p.tiles_y);
+    const int y0 = (r / p.tiles_x) * ST, x0 = (r % p.tiles_x) * ST;
+    __syncthreads();
+    stage_halo(p, halo, img, y0, x0, 0, p.c);
+    if (threadIdx.x < ST * ST) {
+      const int oy = y0 + threadIdx.x / ST, ox = x0 + threadIdx.x % ST;
+      dyl[threadIdx.x] = (oy < p.h && ox < p.w) ? p.dy[((long)img * p.h + oy) * p.w + ox] : 0.f;
+    }
+    __syncthreads();
+    if (act) {
+      const float* hp = halo + ((t / 3) * HT + t % 3) * CS + cc;
+      float s = 0.f;
+      for (int py = half * (ST / 2); py < (half + 1) * (ST / 2); ++py)
+#pragma unroll 8
+        for (int px = 0; px < ST; ++px) s += hp[(py * HT + px) * CS] * dyl[py * ST + px];
+      acc += s;
+    }
+  }
+  __syncthreads();
+  if (half == 1 && act) comb[e] = acc;
+  __syncthreads();
+  if (half == 0 && act) p.part[(long)blockIdx.x * nE + e] = acc + comb[e];
+}
+
+__global__ void skinny_wgrad_reduce_kernel(const float* __restrict__ part, int nb, int per,
+                                           float* __restrict__ dw, int acc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= per) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * per + e];
+  dw[e] = acc ? dw[e] + (float)s : (float)s;
+}
+
+constexpr int SKINNY_WG_BLOCKS = 2048;
+
+}  // namespace pld
+
+using namespace pld;
+
+// eligibility: 3x3 stride-1 'same', single source, no prologue, cout 1, c % 4 == 0
+extern "C" int pld__skinny_eligible(const pld_conv_args* a) {
+  return a && a->cout == 1 && a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 &&
+         a->c2 == 0 && a->in_scale == nullptr && a->c1 % 4 == 0 && a->c1 <= CH &&
+         a->oh == a->h && a->ow == a->w && a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 &&
+         a->pad_l <= 2;
+}
+
+static SkinnyParams mk(const pld_conv_args* a) {
+  SkinnyParams p{};
+  p.x = a->x1;
+  p.n = a->n; p.h = a->h; p.w = a->w; p.c = a->c1;
+  p.pt = a->pad_t; p.pl = a->pad_l;
+  p.tiles_x = (int)cdiv(a->w, ST);
+  p.tiles_y = (int)cdiv(a->h, ST);
+  return p;
+}
+
+extern "C" int pld__skinny_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,
+                               float* y, int accumulate, void* stream) {
+  SkinnyParams p = mk(a);
+  p.wt = w_ohwi;  // [1][3][3][c] == [tap][c]
+  p.bias = bias;
+  p.y = y;
+  p.acc = accumulate;
+  dim3 grid(p.tiles_x, p.tiles_y, p.n);
+  skinny_fwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(p);
+  return check_launch("skinny_fwd_kernel");
+}
+
+extern "C" int pld__skinny_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
+                                 float* dx, int accumulate, void* stream) {
+  SkinnyParams p = mk(a);
+  p.dy = dy;
+  p.wt = w_dgrad;
+  p.y = dx;
+  p.acc = accumulate;
+  dim3 grid(p.tiles_x, p.tiles_y, p.n);
+  skinny_dgrad_kernel<<<grid, 256, 0, as_stream(stream)>>>(p);
+  return check_launch("skinny_dgrad_kernel");
+}
+
+extern "C" size_t pld__skinny_wgrad_ws(const pld_conv_args* a) {
+  return sizeof(float) * (size_t)SKINNY_WG_BLOCKS * 9 * a->c1;
+}
+
+extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float* dw,
+                                 int accumulate, void* ws, void* stream) {
+  SkinnyParams p = mk(a);
+  p.dy = dy;
+  p.part = (float*)ws;
+  const int ntiles = p.tiles_x * p.tiles_y * p.n;
+  const int nb = std::min(SKINNY_WG_BLOCKS, ntiles);
+  hipStream_t st = as_stream(stream);
+  skinny_wgrad_kernel<<<nb, WG_THREADS, 0, st>>>(p);
+  int rc = check_launch("skinny_wgrad_kernel");
+  if (rc) return rc;
+  const int per = 9 * p.c;
+  skinny_wgrad_reduce_kernel<<<cdiv(per, 256), 256, 0, st>>>(p.part, nb, per, dw, accumulate);
+  return check_launch("skinny_wgrad_reduce_kernel");
+}

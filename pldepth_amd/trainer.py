@@ -24,9 +24,14 @@ SAMPLING_TYPES = {0: "thresh", 1: "info", 3: "pure"}  # PLDepth.py:97-108 --samp
 class ReplicaTrainer:
     def __init__(self, input_shape=(448, 448, 3), batch_size=32, ranking_size=5,
                  rankings_per_image=100, sampling_type=1, seed=0, rank=0, world_size=1,
-                 process_group=None, model="ff_effnet", drop_connect=True):
-        if model != "ff_effnet":
+                 process_group=None, model="ff_effnet", drop_connect=True, engine=None,
+                 gpu_sampler=True, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        """gpu_sampler=False: rankings come from the caller (set_rankings), as model.fit feeds
+        y_true batches; otherwise the GPU sampler draws them from (gt, mask) each step."""
+        if model != "ff_effnet" and engine is None:
             raise NotImplementedError(f"model {model!r}: only ff_effnet has a HIP engine yet")
+        self.gpu_sampler = gpu_sampler
+        self.betas = (beta_1, beta_2, epsilon)
         self.B, self.L, self.R = batch_size, ranking_size, rankings_per_image
         self.H, self.W = input_shape[:2]
         self.strategy = SAMPLING_TYPES[sampling_type] if isinstance(sampling_type, int) \
@@ -36,7 +41,8 @@ class ReplicaTrainer:
         self.seed = seed
         dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        self.engine = EffNetFF(input_shape, batch_size, device=dev, seed=seed)
+        self.engine = engine if engine is not None else EffNetFF(input_shape, batch_size,
+                                                                 device=dev, seed=seed)
         self.engine.drop_connect = drop_connect
         B, H, W, L, R = self.B, self.H, self.W, self.L, self.R
         self.n_cand = K.sampler_candidates(R, self.strategy)
@@ -64,13 +70,34 @@ class ReplicaTrainer:
 
     # ------------------------------------------------------------------ data
     def set_batch(self, images, gt, mask):
-        """images [B,H,W,3] in [0,1], gt [B,H,W], mask [B,H,W] (>0 valid) — host or device."""
-        self.x.copy_(torch.as_tensor(images, dtype=torch.float32))
-        self.gt.copy_(torch.as_tensor(gt, dtype=torch.float32))
-        self.mask.copy_(torch.as_tensor(mask, dtype=torch.float32))
+        """images [B,H,W,3] in [0,1], gt [B,H,W], mask [B,H,W] (>0 valid) — host or device.
+        The copies are ordered on the trainer's stream (before the next step's kernels)."""
+        with torch.cuda.stream(self.stream):
+            if images is not None:
+                self.x.copy_(torch.as_tensor(images, dtype=torch.float32).reshape(self.x.shape))
+            if gt is not None:
+                self.gt.copy_(torch.as_tensor(gt, dtype=torch.float32).reshape(self.gt.shape))
+            if mask is not None:
+                self.mask.copy_(torch.as_tensor(mask, dtype=torch.float32)
+                                .reshape(self.mask.shape))
+
+    def set_rankings(self, y_true):
+        """External rankings [B, R, L, 2] (float32 flat index, depth) for the next step."""
+        y = torch.as_tensor(y_true, dtype=torch.float32)
+        R = y.numel() // (2 * self.B * self.L)
+        if R != self.R_out or self.y_true.numel() != y.numel():
+            if self.graphs is not None:
+                raise ValueError("ranking count changed after graph capture")
+            self.R_out = R
+            self.y_true = torch.empty(self.B, R, self.L, 2, device=self.device)
+            self.nll = torch.empty(self.B * R, device=self.device)
+        with torch.cuda.stream(self.stream):
+            self.y_true.copy_(y.reshape(self.y_true.shape))
 
     # ------------------------------------------------------------------ phases
     def _sample(self):
+        if not self.gpu_sampler:
+            return
         K.sampler_compact(self.mask, self.gt, self.valid_idx, self.nvalid, self.minmax)
         K.sampler_draw(self.nvalid, self.n_cand, self.L, self.seed, self.step_dev,
                        self.rank * self.B, self.draws)
@@ -86,15 +113,18 @@ class ReplicaTrainer:
 
     def _update(self):
         eng = self.engine
+        b1, b2, eps = self.betas
         K.adam_amsgrad_dev(eng.params.buf, eng.grads.buf, self.m, self.v, self.vhat, self.lr_dev,
-                           self.step_dev, grad_scale=1.0 / self.world)
+                           self.step_dev, b1, b2, eps, grad_scale=1.0 / self.world)
         eng.refresh_trainable()
         K.step_increment(self.step_dev)
 
     def _allreduce(self):
         if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.engine.grads.buf, group=self.pg)
+            if not hasattr(self, "_reducer"):
+                from .dp import GradientAllReducer
+                self._reducer = GradientAllReducer(self.engine.grads.buf, self.pg)
+            self._reducer()
 
     # ------------------------------------------------------------------ driving
     def step_eager(self, lr):

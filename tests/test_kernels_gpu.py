@@ -88,6 +88,13 @@ CONV_CASES = [
     (2, 16, 16, 32, 0, 3, 1, 1, True, False),      # final conv: Cout=1
     (1, 14, 14, 64, 64, 3, 1, 130, True, True),    # concat + prologue on source 1
     (2, 6, 6, 1280, 0, 3, 1, 672, True, False),    # c0-like channel counts
+    (2, 37, 45, 16, 0, 3, 1, 1, True, False),      # Cout=1 direct kernels, ragged tiles
+    (1, 40, 33, 32, 0, 3, 1, 1, False, False),
+    (1, 10, 10, 12, 0, 3, 1, 1, True, False),      # Cout=1, C not a multiple of 8
+    (2, 12, 12, 48, 48, 3, 1, 144, True, False),   # N=144 (128x160 tile), dgrad N=96
+    (1, 9, 9, 32, 64, 3, 1, 240, True, False),     # N=240; dgrad splits 32|64
+    (1, 8, 8, 96, 0, 3, 1, 224, True, False),      # N=224 exact tile
+    (3, 5, 7, 320, 0, 1, 1, 1280, False, False),   # top conv shape class
 ]
 
 
