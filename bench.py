@@ -161,6 +161,8 @@ def main():
     ap.add_argument("--sampling-type", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tile-cache", default="",
+                    help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -186,9 +188,14 @@ def main():
     tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
                  torch.from_numpy(mask).cuda())
     lr = 0.01
-    # first step eager: sizes every workspace, then capture the graph(s)
+    from pldepth_amd import kernels as K
+    if a.tile_cache and os.path.exists(a.tile_cache):
+        K.load_tile_cache(a.tile_cache)
+    # first step eager: tunes conv schedules, sizes every workspace, then capture the graph(s)
     tr.step_eager(lr)
     torch.cuda.synchronize()
+    if a.tile_cache and rank == 0:
+        K.save_tile_cache(a.tile_cache)
     if not a.no_graph:
         tr.capture()
     for _ in range(max(a.warmup - 1, 0)):

@@ -97,7 +97,21 @@ typedef struct pld_conv_args {
   const float* in_scale;
   const float* in_shift;
   int in_act;
+  /* implicit-GEMM schedule: -1 = built-in heuristic, else an index < pld_conv_num_tiles()
+   * selecting a block tile and whether the GEMM's K is split across workgroups (callers
+   * autotune per layer shape; every schedule computes the same result up to fp32 summation
+   * order) */
+  int tile;
+  /* caller workspace for split-K partial slabs of the forward / dgrad GEMMs (size from
+   * pld_conv2d_{fwd,dgrad}_workspace_size; may be NULL when that size is 0) */
+  void* ws;
+  size_t ws_bytes;
 } pld_conv_args;
+
+/* number of implicit-GEMM schedules selectable through pld_conv_args.tile */
+int pld_conv_num_tiles(void);
+size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a);
+size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a);
 
 /* forward: y[n][oh][ow][cout] (+)= conv(x, W) + bias.  w_ohwi = native layout
  * [cout][kh][kw][c1+c2] (pld_filter_to_native).  bias may be NULL. */

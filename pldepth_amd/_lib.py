@@ -30,7 +30,8 @@ class ConvArgs(C.Structure):
         ("n", I32), ("h", I32), ("w", I32),
         ("kh", I32), ("kw", I32), ("sh", I32), ("sw", I32), ("pad_t", I32), ("pad_l", I32),
         ("oh", I32), ("ow", I32), ("cout", I32),
-        ("in_scale", P), ("in_shift", P), ("in_act", I32),
+        ("in_scale", P), ("in_shift", P), ("in_act", I32), ("tile", I32),
+        ("ws", P), ("ws_bytes", SZ),
     ]
 
 
@@ -48,6 +49,9 @@ _SIGS = {
     "pld_conv2d_dgrad": (I32, [C.POINTER(ConvArgs), P, P, P, I32, P, I32, P]),
     "pld_conv2d_wgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_wgrad": (I32, [C.POINTER(ConvArgs), P, P, I32, P, SZ, P]),
+    "pld_conv_num_tiles": (I32, []),
+    "pld_conv2d_fwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
+    "pld_conv2d_dgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_filter_to_native": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_filter_to_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_channel_reduce_workspace_size": (SZ, [I64, I32]),
@@ -79,7 +83,8 @@ _SIGS = {
 }
 
 # functions returning a value rather than a status
-_NON_STATUS = {"pld_last_error", "pld_version", "pld_conv2d_wgrad_workspace_size",
+_NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles",
+               "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates"}
 

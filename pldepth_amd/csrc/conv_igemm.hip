@@ -22,6 +22,7 @@
 // Roofline: MFMA-bound for the decoder shapes (fp32 peak 157.3 TF/s), HBM-bound for skinny
 // encoder 1x1 convs (K = 16..40).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
   const int n0 = blockIdx.y * BN;
 
   int kt_begin = 0, kt_end = (p.K + BK - 1) / BK;
-  if (MODE == MODE_WGRAD) {
+  if (p.ktiles_per_split > 0) {  // split-K: this workgroup's slice of the reduction
     kt_begin = blockIdx.z * p.ktiles_per_split;
     kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
   }
@@ -382,7 +383,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
 #undef Bs
   // ------------------------------------------------------------------ epilogue
   float* out1 = p.out1;
-  if (MODE == MODE_WGRAD) out1 += (long)blockIdx.z * p.zstride;
+  if (p.zstride > 0) {  // split-K partial slab [z][M][N], reduced (+bias, routing) afterwards
+    out1 += (long)blockIdx.z * p.zstride;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n0 + wn * WTN + b * 32 + l32;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < p.M) out1[(long)row * p.N + col] = acc[a][b][r];
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -415,6 +431,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     float s = 0.f;
     for (int z = 0; z < splits; ++z) s += ws[(long)z * n + i];
     dw[i] = acc ? dw[i] + s : s;
+  }
+}
+
+// ordered split-K reduction of forward / dgrad slabs with bias and two-destination routing
+__global__ __launch_bounds__(256) void splitk_out_kernel(const float* __restrict__ ws, int splits,
+                                                         long M, int N, const float* bias,
+                                                         float* out1, int ld1, int acc1,
+                                                         float* out2, int ld2, int acc2,
+                                                         int split) {
+  const long n = M * N;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[(long)z * n + i];
+    const long row = i / N;
+    const int col = (int)(i - row * N);
+    if (bias) s += bias[col];
+    if (col < split) {
+      float* d = out1 + row * ld1 + col;
+      *d = acc1 ? *d + s : s;
+    } else {
+      float* d = out2 + row * ld2 + (col - split);
+      *d = acc2 ? *d + s : s;
+    }
   }
 }
 
@@ -458,10 +498,17 @@ static const TileCfg kTiles[] = {
 
 // estimated relative time: padded MFMA work per block x waves of blocks over 256 CUs,
 // discounted by the per-wave tile count (fragment reuse)
-static int choose_tile(long M, long N, long K, int splits) {
+static constexpr int kNumCfg = (int)(sizeof(kTiles) / sizeof(kTiles[0]));
+static constexpr int kNumTiles = 2 * kNumCfg;  // x {no split-K, split-K} for fwd / dgrad
+
+static int choose_tile(long M, long N, long K, int splits, int requested = -1) {
+  if (requested >= 0 && requested < kNumTiles) return requested % kNumCfg;
+  // measurement override (tile sweeps): PLD_CONV_TILE=<index into kTiles>
+  static const char* ov = getenv("PLD_CONV_TILE");
+  if (ov && *ov) return atoi(ov);
   int best = 0;
   double best_t = 1e300;
-  for (int i = 0; i < (int)(sizeof(kTiles) / sizeof(kTiles[0])); ++i) {
+  for (int i = 0; i < kNumCfg; ++i) {
     const TileCfg& t = kTiles[i];
     const long blocks = (long)cdiv(M, t.bm) * cdiv(N, t.bn) * splits;
     const int per_wave = t.tm * t.tn;
@@ -545,6 +592,55 @@ extern "C" size_t pld__skinny_wgrad_ws(const pld_conv_args* a);
 extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float* dw,
                                  int accumulate, void* ws, void* stream);
 
+// split-K plan for a forward / dgrad GEMM under schedule `tile`: enough workgroups for ~3 per
+// CU, >= 16 K-steps each; the split-K schedules (tile >= kNumCfg) only
+static void fwd_split_plan(long M, long N, long K, int tile, int& cfg, int& splits,
+                           int& kt_per) {
+  cfg = choose_tile(M, N, K, 1, tile);
+  const bool allow = tile >= kNumCfg;
+  const long ktiles = (K + BK - 1) / BK;
+  const long blocks = (long)cdiv(M, kTiles[cfg].bm) * cdiv(N, kTiles[cfg].bn);
+  long s = 1;
+  if (allow) {
+    s = std::max<long>(1, (768 + blocks - 1) / blocks);
+    s = std::min<long>(s, std::max<long>(1, ktiles / 16));
+    s = std::min<long>(s, 16);
+  }
+  kt_per = (int)((ktiles + s - 1) / s);
+  splits = (int)((ktiles + kt_per - 1) / kt_per);
+}
+
+static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void* ws,
+                        size_t ws_bytes, hipStream_t st, const char* who) {
+  int cfg, splits, kt_per;
+  fwd_split_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+  if (splits == 1) {
+    p.ktiles_per_split = 0;
+    p.zstride = 0;
+    return launch_igemm<MODE_FWD>(p, vec, vec16, 1, cfg, st);
+  }
+  const size_t need = sizeof(float) * (size_t)splits * p.M * p.N;
+  PLD_CHECK_ARG(ws && ws_bytes >= need, "%s: split-K workspace %zu < %zu bytes", who, ws_bytes,
+                need);
+  GemmConvParams q = p;
+  q.ktiles_per_split = kt_per;
+  q.zstride = (long)p.M * p.N;
+  q.out1 = (float*)ws;
+  int rc = launch_igemm<MODE_FWD>(q, vec, vec16, splits, cfg, st);
+  if (rc) return rc;
+  const long n = (long)p.M * p.N;
+  splitk_out_kernel<<<std::min<unsigned>(cdiv(n, 256), 8192), 256, 0, st>>>(
+      (const float*)ws, splits, p.M, p.N, p.bias, p.out1, p.ld1, p.acc1, p.out2, p.ld2, p.acc2,
+      p.split);
+  return check_launch("splitk_out_kernel");
+}
+
+static size_t fwd_ws_bytes(long M, long N, long K, int tile) {
+  int cfg, splits, kt_per;
+  fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
+  return splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+}
+
 extern "C" int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout,
                                     float* w_ohwi, void* stream) {
   PLD_CHECK_ARG(w_hwio && w_ohwi && kh > 0 && kw > 0 && cin > 0 && cout > 0,
@@ -586,8 +682,24 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
                    (!p.x2 || aligned16(p.x2)) && aligned16(w_ohwi) &&
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
   const bool vec16 = vec && (p.c1 % 16 == 0) && (p.c2 % 16 == 0);
-  return launch_igemm<MODE_FWD>(p, vec, vec16, 1, choose_tile(p.M, p.N, p.K, 1),
-                                as_stream(stream));
+  return run_fwd_gemm(p, vec, vec16, a->tile, a->ws, a->ws_bytes, as_stream(stream),
+                      "pld_conv2d_fwd");
+}
+
+extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
+
+extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
+  if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
+  if (pld__skinny_eligible(a)) return 0;
+  return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
+                      (long)a->kh * a->kw * (a->c1 + a->c2), a->tile);
+}
+
+extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
+  if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->h <= 0 || a->w <= 0) return 0;
+  if (pld__skinny_eligible(a)) return 0;
+  return fwd_ws_bytes((long)a->n * a->h * a->w, a->c1 + a->c2, (long)a->kh * a->kw * a->cout,
+                      a->tile);
 }
 
 extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
@@ -632,8 +744,8 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   p.split = a->c1;
   const bool vec = (p.c1 % 4 == 0) && aligned16(dy) && aligned16(w_dgrad);
   const bool vec16 = vec && (p.c1 % 16 == 0);
-  return launch_igemm<MODE_FWD>(p, vec, vec16, 1, choose_tile(p.M, p.N, p.K, 1),
-                                as_stream(stream));
+  return run_fwd_gemm(p, vec, vec16, a->tile, a->ws, a->ws_bytes, as_stream(stream),
+                      "pld_conv2d_dgrad");
 }
 
 static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& splits,
@@ -643,7 +755,7 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
   K = (long)a->n * a->oh * a->ow;
   const long ktiles = (K + BK - 1) / BK;
   // pick the tile for an unsplit GEMM, then split K until ~3 blocks per CU
-  cfg = choose_tile(M, N, K, 1);
+  cfg = choose_tile(M, N, K, 1, a->tile);
   const long tiles = (long)cdiv(M, kTiles[cfg].bm) * cdiv(N, kTiles[cfg].bn);
   long s = std::max<long>(1, (768 + tiles - 1) / tiles);
   s = std::min<long>(s, std::max<long>(1, ktiles / 8));  // >= 8 k-steps per block

@@ -165,13 +165,22 @@ __global__ __launch_bounds__(WG_THREADS) void skinny_wgrad_kernel(SkinnyParams p
   if (half == 0 && act) p.part[(long)blockIdx.x * nE + e] = acc + comb[e];
 }
 
-__global__ void skinny_wgrad_reduce_kernel(const float* __restrict__ part, int nb, int per,
-                                           float* __restrict__ dw, int acc) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= per) return;
+// one workgroup per output: strided partial sums then a fixed-shape tree (deterministic)
+__global__ __launch_bounds__(256) void skinny_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                  int nb, int per,
+                                                                  float* __restrict__ dw,
+                                                                  int acc) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * per + e];
-  dw[e] = acc ? dw[e] + (float)s : (float)s;
+  for (int b = threadIdx.x; b < nb; b += 256) s += part[(long)b * per + e];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dw[e] = acc ? dw[e] + (float)red[0] : (float)red[0];
 }
 
 constexpr int SKINNY_WG_BLOCKS = 2048;
@@ -238,6 +247,6 @@ extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float*
   int rc = check_launch("skinny_wgrad_kernel");
   if (rc) return rc;
   const int per = 9 * p.c;
-  skinny_wgrad_reduce_kernel<<<cdiv(per, 256), 256, 0, st>>>(p.part, nb, per, dw, accumulate);
+  skinny_wgrad_reduce_kernel<<<per, 256, 0, st>>>(p.part, nb, per, dw, accumulate);
   return check_launch("skinny_wgrad_reduce_kernel");
 }

@@ -4,6 +4,7 @@ PyTorch is plumbing here: tensors provide device memory and the current HIP stre
 computation is a call into libpldepth_hip.so. Nothing here falls back to torch math.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -84,9 +85,11 @@ class Graph:
 
     def capture(self, fn):
         lib().pld_graph_begin(stream())
+        _CAPTURING[0] = True
         try:
             fn()
         finally:
+            _CAPTURING[0] = False
             h = C.c_void_p()
             lib().pld_graph_end(stream(), C.byref(h))
         self.exec = h
@@ -126,6 +129,7 @@ def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None,
     a.in_scale = None if in_scale is None else in_scale.data_ptr()
     a.in_shift = None if in_shift is None else in_shift.data_ptr()
     a.in_act = ACT[in_act]
+    a.tile = -1
     return a
 
 
@@ -145,18 +149,119 @@ def filter_to_dgrad(w_hwio, out=None):
     return out
 
 
+# ---- per-shape tile autotuning (eager only; the choice never changes results) ----
+AUTOTUNE = os.environ.get("PLD_AUTOTUNE", "1") != "0"
+_TILE_CACHE = {}
+_CAPTURING = [False]
+
+
+def load_tile_cache(path):
+    """Merge schedules tuned by an earlier run (JSON written by save_tile_cache)."""
+    import json
+    with open(path) as f:
+        for k, v in json.load(f):
+            _TILE_CACHE[tuple(k)] = int(v)
+
+
+def save_tile_cache(path):
+    import json
+    with open(path, "w") as f:
+        json.dump([[list(k), v] for k, v in _TILE_CACHE.items()], f)
+
+
+def _shape_key(mode, a):
+    return (mode, a.n, a.h, a.w, a.c1, a.c2, a.kh, a.kw, a.sh, a.sw, a.pad_t, a.pad_l, a.oh,
+            a.ow, a.cout, bool(a.in_scale))
+
+
+def _skinny(a):
+    return (a.cout == 1 and a.kh == 3 and a.kw == 3 and a.sh == 1 and a.c2 == 0
+            and not a.in_scale and a.c1 % 4 == 0 and a.c1 <= 32)
+
+
+def _tune(mode, a, run):
+    """run(tile) launches the conv into scratch outputs; returns the fastest schedule index
+    (tile x split-K for fwd/dgrad; wgrad sizes its own split, so only the tile is searched)."""
+    key = _shape_key(mode, a)
+    if key in _TILE_CACHE:
+        return _TILE_CACHE[key]
+    if not AUTOTUNE or _CAPTURING[0] or _skinny(a):
+        return -1
+    best, best_t = -1, float("inf")
+    st = torch.cuda.current_stream()
+    n = lib().pld_conv_num_tiles()
+    for t in range(n // 2 if mode == "wgrad" else n):
+        run(t)  # warm-up (also sizes the workspace)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        run(t)
+        run(t)
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        if ms < best_t:
+            best, best_t = t, ms
+    _TILE_CACHE[key] = best
+    return best
+
+
+def _splitk_ws(args, fn):
+    need = fn(C.byref(args))
+    if need:
+        ws = workspace(need, "splitk")
+        args.ws, args.ws_bytes = ws.data_ptr(), ws.numel()
+    else:
+        args.ws, args.ws_bytes = None, 0
+
+
 def conv2d_fwd(args, w_native, bias, y, accumulate=False):
+    if args.tile < 0:
+        scratch = None
+
+        def run(t):
+            nonlocal scratch
+            scratch = torch.empty_like(y) if scratch is None else scratch
+            args.tile = t
+            _splitk_ws(args, lib().pld_conv2d_fwd_workspace_size)
+            lib().pld_conv2d_fwd(C.byref(args), ptr(w_native), ptr(bias), ptr(scratch), 0,
+                                 stream())
+        args.tile = _tune("fwd", args, run)
+    _splitk_ws(args, lib().pld_conv2d_fwd_workspace_size)
     lib().pld_conv2d_fwd(C.byref(args), ptr(w_native), ptr(bias), ptr(y), int(accumulate),
                          stream())
     return y
 
 
 def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
+    if args.tile < 0:
+        s1 = s2 = None
+
+        def run(t):
+            nonlocal s1, s2
+            s1 = torch.empty_like(dx1) if s1 is None else s1
+            s2 = (torch.empty_like(dx2) if dx2 is not None else None) if s2 is None else s2
+            args.tile = t
+            _splitk_ws(args, lib().pld_conv2d_dgrad_workspace_size)
+            lib().pld_conv2d_dgrad(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(s1), 0, ptr(s2), 0,
+                                   stream())
+        args.tile = _tune("dgrad", args, run)
+    _splitk_ws(args, lib().pld_conv2d_dgrad_workspace_size)
     lib().pld_conv2d_dgrad(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(dx1), int(acc1), ptr(dx2),
                            int(acc2), stream())
 
 
 def conv2d_wgrad(args, dy, dw, accumulate=False):
+    if args.tile < 0:
+        sdw = None
+
+        def run(t):
+            nonlocal sdw
+            sdw = torch.empty_like(dw) if sdw is None else sdw
+            args.tile = t
+            need = lib().pld_conv2d_wgrad_workspace_size(C.byref(args))
+            ws = workspace(need, "wgrad") if need else None
+            lib().pld_conv2d_wgrad(C.byref(args), ptr(dy), ptr(sdw), 0, ptr(ws), need, stream())
+        args.tile = _tune("wgrad", args, run)
     need = lib().pld_conv2d_wgrad_workspace_size(C.byref(args))
     ws = workspace(need, "wgrad") if need else None
     lib().pld_conv2d_wgrad(C.byref(args), ptr(dy), ptr(dw), int(accumulate), ptr(ws), need,

@@ -39,6 +39,17 @@ def test_host_only_entry_points():
         raise AssertionError("expected PLDError")
     a = _lib.ConvArgs()
     assert lib.pld_conv2d_wgrad_workspace_size(C.byref(a)) == 0  # invalid geometry
+    assert lib.pld_conv2d_fwd_workspace_size(C.byref(a)) == 0
+    assert lib.pld_conv2d_dgrad_workspace_size(C.byref(a)) == 0
+    # split-K schedules of a deep, small-M GEMM need a slab workspace; plain ones do not
+    a.n, a.h, a.w, a.c1, a.kh, a.kw, a.sh, a.sw = 1, 7, 7, 1024, 3, 3, 1, 1
+    a.pad_t = a.pad_l = 1
+    a.oh, a.ow, a.cout = 7, 7, 64
+    nt = lib.pld_conv_num_tiles()
+    a.tile = 0
+    assert lib.pld_conv2d_fwd_workspace_size(C.byref(a)) == 0
+    a.tile = nt // 2
+    assert lib.pld_conv2d_fwd_workspace_size(C.byref(a)) >= 2 * 49 * 64 * 4
 
 
 def test_header_documents_reference_replacements():

@@ -12,6 +12,9 @@ import torch.nn.functional as F
 from oracle import effnet as OE
 from oracle import listmle as LM
 from oracle import sampler as S
+import ctypes as C
+
+from pldepth_amd import _lib
 from pldepth_amd import kernels as K
 
 pytestmark = pytest.mark.gpu
@@ -162,6 +165,52 @@ def test_conv_fwd_dgrad_wgrad(cuda, case):
         assert rel_err(dx1, x1r.grad) < 1e-5, rel_err(dx1, x1r.grad)
         if x2 is not None:
             assert rel_err(dx2 - 1.0, x2r.grad) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 96, 32, 3, 1, 64, True),
+                                  (1, 9, 11, 64, 0, 1, 1, 320, False)])
+def test_conv_every_schedule(cuda, case):
+    """Each tile x split-K schedule computes the same conv (fwd with bias routing, dgrad into
+    two concat destinations with accumulate)."""
+    n, h, w, c1, c2, k, s, cout, has_bias = case
+    torch.manual_seed(7)
+    x1 = torch.randn(n, h, w, c1, dtype=torch.float64)
+    x2 = torch.randn(n, h, w, c2, dtype=torch.float64) if c2 else None
+    wt = torch.randn(k, k, c1 + c2, cout, dtype=torch.float64) / np.sqrt(k * k * (c1 + c2))
+    b = torch.randn(cout, dtype=torch.float64) if has_bias else None
+    pt, pb, _ = OE.same_pad(h, k, 1)
+    pl, pr, _ = OE.same_pad(w, k, 1)
+    x1r = x1.clone().requires_grad_(True)
+    x2r = x2.clone().requires_grad_(True) if x2 is not None else None
+    y_ref = _ref_conv(x1r, x2r, wt, b, k, 1, pt, pb, pl, pr)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    gx1, gx2, gw = dev(x1, cuda), (dev(x2, cuda) if c2 else None), dev(wt, cuda)
+    wn, wd = K.filter_to_native(gw), K.filter_to_dgrad(gw)
+    gb, gdy = (dev(b, cuda) if has_bias else None), dev(dy, cuda)
+    n_sched = _lib.lib().pld_conv_num_tiles()
+    assert n_sched >= 2 and n_sched % 2 == 0
+    for t in range(n_sched):
+        args = K.conv_args(gx1, gx2, k, k, 1, pt, pl, h, w, cout)
+        args.tile = t
+        y = torch.full((n, h, w, cout), 0.5, device=cuda)
+        K.conv2d_fwd(args, wn, gb, y, accumulate=True)
+        dx1 = torch.empty_like(gx1)
+        dx2 = torch.full_like(gx2, 1.0) if c2 else None
+        K.conv2d_dgrad(args, gdy, wd, dx1, dx2, acc2=True)
+        torch.cuda.synchronize()
+        assert rel_err(y - 0.5, y_ref) < 1e-5, (t, rel_err(y - 0.5, y_ref))
+        assert rel_err(dx1, x1r.grad) < 1e-5, t
+        if c2:
+            assert rel_err(dx2 - 1.0, x2r.grad) < 1e-5, t
+    # a split-K schedule without a workspace fails loudly
+    args = K.conv_args(gx1, gx2, k, k, 1, pt, pl, h, w, cout)
+    args.tile = n_sched - 1
+    need = _lib.lib().pld_conv2d_fwd_workspace_size(C.byref(args))
+    if need:
+        with pytest.raises(_lib.PLDError):
+            _lib.lib().pld_conv2d_fwd(C.byref(args), wn.data_ptr(), None,
+                                      torch.empty(n, h, w, cout, device=cuda).data_ptr(), 0, None)
 
 
 def test_channel_sum(cuda):
