@@ -81,20 +81,36 @@ def profile_conv(trainer, lr):
     return fl, sec, len(recs)
 
 
-def cpu_baseline(H, W, L, R, seconds_budget=25.0):
+def cpu_baseline(H, W, L, R, model="ff_effnet", seconds_budget=25.0):
     """The oracle (torch-CPU fp32 restatement of the full step + numpy sampler restatement),
     8 threads as the reference's init_tensorflow(num_threads=8), on a bounded sample."""
     sys.path.insert(0, ROOT)
-    from oracle import effnet as OE
     from oracle import listmle as LM
     from oracle import sampler as S
-    from pldepth_amd.models.effnet_ff import FlatStore  # noqa: F401  (names only)
     torch.set_num_threads(8)
     B = 2
     x, gt, mask = synthetic_batch(B, H, W, seed=123)
-    w = _cpu_weights(H, W)
+    if model == "ff_effnet":
+        from oracle import effnet as OM
+        w = _cpu_weights(H, W)
+    else:
+        from oracle import redweb as OM
+        from pldepth_amd.models.redweb_ff import preprocess_input
+        x = preprocess_input(x)
+        rng = np.random.default_rng(0)
+        w = {}
+        for n, shp, _ in OM.param_specs():
+            if n.endswith(("/gamma", "moving_variance")):
+                w[n] = np.ones(shp, np.float32)
+            elif len(shp) == 1:
+                w[n] = np.zeros(shp, np.float32)
+            else:
+                lim = np.sqrt(6.0 / (shp[0] * shp[1] * (shp[2] + shp[3])))
+                w[n] = rng.uniform(-lim, lim, shp).astype(np.float32)
     P = {k: torch.tensor(v) for k, v in w.items()}
-    names = sorted(OE.trainable_names(P))
+    names = sorted(OM.trainable_names(P))
+    fwd = (lambda Q, xx: OM.forward(Q, xx)) if model == "ff_effnet" else \
+        (lambda Q, xx: OM.forward(Q, xx, preprocessed=True))
     from oracle.adam import adam_amsgrad_step
     adam = {k: [np.zeros(P[k].shape, np.float32) for _ in range(3)] for k in names}
     np.random.seed(0)
@@ -103,7 +119,7 @@ def cpu_baseline(H, W, L, R, seconds_budget=25.0):
         ys = [S.sample_masked_point_batch("info", mask[b], gt[b], R, L)[0] for b in range(B)]
         y = np.stack(ys)
         Q = {k: (v.clone().requires_grad_(True) if k in names else v) for k, v in P.items()}
-        out = OE.forward(Q, torch.tensor(x))
+        out = fwd(Q, torch.tensor(x))
         loss, dpred = LM.hourglass_nll(y, out.detach().numpy(), B, L)
         out.backward(torch.tensor(dpred, dtype=torch.float32))
         for k in names:  # Adam-AMSGrad (oracle/adam.py) on every trainable tensor
@@ -121,7 +137,7 @@ def cpu_baseline(H, W, L, R, seconds_budget=25.0):
         n_steps += 1
     return {"value": B * n_steps / t_total, "unit": "images/s", "cores": 8, "kind": "port",
             "sample": f"{n_steps} timed full train steps after 1 warm-up (numpy Info sampler + "
-                      f"torch-CPU fp32 ff_effnet fwd/bwd + ListMLE + Adam-AMSGrad), batch {B}, "
+                      f"torch-CPU fp32 {model} fwd/bwd + ListMLE + Adam-AMSGrad), batch {B}, "
                       f"{H}x{W}, L={L}, R={R}, torch.set_num_threads(8)"}
 
 
@@ -159,6 +175,8 @@ def main():
     ap.add_argument("--ranking-size", type=int, default=5)
     ap.add_argument("--rankings-per-image", type=int, default=100)
     ap.add_argument("--sampling-type", type=int, default=1)
+    ap.add_argument("--model", default="ff_effnet", choices=["ff_effnet", "ff_redweb"],
+                    help="ff_redweb = the ResNet-50 backbone (BASELINE cfg3 'ff_resnet')")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tile-cache", default="",
@@ -183,8 +201,10 @@ def main():
     H = W = a.size
     B, L, R = a.batch, a.ranking_size, a.rankings_per_image
     tr = ReplicaTrainer((H, W, 3), B, L, R, a.sampling_type, seed=0, rank=rank,
-                        world_size=world, process_group=pg)
+                        world_size=world, process_group=pg, model=a.model)
     x, gt, mask = synthetic_batch(B, H, W, seed=1000 + rank)
+    if a.model == "ff_redweb":
+        x = tr.engine.preprocess(x)  # the data pipeline's caffe preprocessing (PLDepth.py:169)
     tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
                  torch.from_numpy(mask).cuda())
     lr = 0.01
@@ -242,10 +262,10 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (U[0,1) RGB, smooth 8-bit depth, Bernoulli(0.9) mask; Keras-default "
                 "random-init weights)",
-        "config": {"workload": f"ff_effnet train step {H}x{W}, per-GPU batch {B}, "
+        "config": {"workload": f"{a.model} train step {H}x{W}, per-GPU batch {B}, "
                                f"ranking_size {L}, rankings_per_image {R}, "
                                f"sampler {tr.strategy}, Adam-AMSGrad",
-                   "model": "ff_effnet", "global_batch": world * B, "input": f"{H}x{W}",
+                   "model": a.model, "global_batch": world * B, "input": f"{H}x{W}",
                    "ranking_size": L, "rankings_per_image": R,
                    "parallelism": f"dp{world}", "graph": not a.no_graph},
         "roofline": {
@@ -258,7 +278,7 @@ def main():
         "loss": loss,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(H, W, L, R)
+        out["cpu_baseline"] = cpu_baseline(H, W, L, R, a.model)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

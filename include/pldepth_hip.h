@@ -118,7 +118,9 @@ size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a);
 int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias, float* y,
                    int accumulate, void* stream);
 
-/* input gradient for stride-1 convolutions: dx = conv^T(dy, W).  w_dgrad = native layout
+/* input gradient: dx = conv^T(dy, W) for stride-1 convolutions and for strided 1x1 unpadded
+ * ones (the ResNet-50 downsampling / projection convs, redweb.py:410 -> keras resnet block1;
+ * computed as a GEMM into workspace then scattered to the stride grid).  w_dgrad = native layout
  * [c1+c2][kh][kw][cout] with the taps flipped (pld_filter_to_dgrad).  dx1 receives channels
  * [0,c1), dx2 channels [c1,c1+c2); each is overwritten or accumulated per its flag. */
 int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad, float* dx1,
@@ -165,6 +167,19 @@ int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float
                const float* gate, const float* addn, int hw, float* dx, int dx_accumulate,
                float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
 
+/* residual forms (ResNet-50 blocks `Add -> ReLU`, keras resnet block1; ReDWeb
+ * BottleneckConvLayer `out += residual; relu` redweb.py:137-165 and FeatureFusionLayer
+ * `x_left + x_up` redweb.py:270):  y = act(bn(x) + res);  backward: dz = dy*act'(bn(x)+res),
+ * dgamma/dbeta/dx as pld_bn_bwd, and dres (=|+=) dz (the residual branch's gradient; NULL to
+ * skip).  dx may be NULL when only dres and the parameter gradients are wanted. */
+int pld_bn_add_apply(const float* x, int64_t rows, int c, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const float* res, int act, float* y,
+                     void* stream);
+int pld_bn_add_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                   const float* invstd, const float* gamma, const float* beta, const float* res,
+                   int act, float* dx, int dx_accumulate, float* dres, int dres_accumulate,
+                   float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
+
 /* inference-mode BN (Keras BatchNormalization, training=False): scale = gamma/sqrt(mvar+eps),
  * shift = beta - mmean*scale, for pld_channel_affine_act / the conv prologue */
 int pld_bn_inference_coeffs(const float* gamma, const float* beta, const float* moving_mean,
@@ -177,6 +192,15 @@ int pld_bn_inference_coeffs(const float* gamma, const float* beta, const float* 
 /* y = act(x*scale[c] + shift[c]) (input normalisation, bias+act) over [rows][c] */
 int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
                            const float* shift, int act, float* y, void* stream);
+/* ZeroPadding2D(pad) + MaxPooling2D(k, s) (ResNet-50 stem pool1, redweb.py:410): windows read
+ * zeros outside the input; argmax [n][oh][ow][c] u8 = first maximal tap (row-major) or NULL;
+ * bwd gathers dy onto those taps: dx [n][h][w][c] (=|+=). */
+int pld_maxpool2d_fwd(const float* x, int n, int h, int w, int c, int k, int s, int pad_t,
+                      int pad_l, int oh, int ow, float* y, uint8_t* argmax, void* stream);
+int pld_maxpool2d_bwd(const float* dy, const uint8_t* argmax, int n, int h, int w, int c, int k,
+                      int s, int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
+                      void* stream);
+
 /* UpSampling2D(interpolation='bilinear') x2, half-pixel centres (pl_hourglass.py:62..94):
  * x [n][h][w][c] -> y [n][2h][2w][c];  bwd: dx [n][h][w][c] (=|+=) adjoint(dy) */
 int pld_upsample2x_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream);

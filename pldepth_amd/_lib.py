@@ -60,6 +60,12 @@ _SIGS = {
     "pld_bn_apply": (I32, [P, I64, I32, P, P, P, P, I32, P, I32, P, P]),
     "pld_bn_bwd": (I32, [P, P, I64, I32, P, P, P, P, I32, P, P, I32, P, I32, P, P, I32, P, P]),
     "pld_channel_affine_act": (I32, [P, I64, I32, P, P, I32, P, P]),
+    "pld_bn_add_apply": (I32, [P, I64, I32, P, P, P, P, P, I32, P, P]),
+    "pld_bn_add_bwd": (I32, [P, P, I64, I32, P, P, P, P, P, I32, P, I32, P, I32, P, P, I32, P,
+                             P]),
+    "pld_maxpool2d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P]),
+    "pld_maxpool2d_bwd": (I32, [P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32,
+                                P]),
     "pld_upsample2x_fwd": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_upsample2x_bwd": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "pld_residual_add": (I32, [P, P, P, I32, I64, P, P]),

@@ -33,6 +33,7 @@ struct RedParams {
   int act;
   const float* gate;
   const float* addn;
+  const float* res;  // residual added before the activation (ResNet / ReDWeb blocks), or NULL
   FastDiv dHW;
   double* partial;  // [gridDim.x][C][2]
 };
@@ -94,10 +95,14 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
         if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
         if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
+        float rv[VW];
+#pragma unroll
+        for (int u = 0; u < VW; ++u) rv[u] = 0.f;
+        if (p.res) ld<VW>(p.res + r * p.C + c0, rv);
 #pragma unroll
         for (int u = 0; u < VW; ++u) {
           const float xh = (xv[u] - mean[u]) * inv[u];
-          const float z = xh * gam[u] + bet[u];
+          const float z = (xh * gam[u] + bet[u]) + rv[u];
           const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
           s0[u] += (double)dz;
           s1[u] += (double)dz * (double)xh;
@@ -235,6 +240,7 @@ struct ApplyParams {
   const float* shift;
   int act;
   const float* gate;
+  const float* res;
   FastDiv dHW;
   FastDiv dCV;
   float* y;
@@ -268,6 +274,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
 #pragma unroll
       for (int u = 0; u < VW; ++u) xv[u] = xv[u] * a[u] + b[u];
     }
+    if (p.res) {
+      float rv[VW];
+      ld<VW>(p.res + e * VW, rv);
+#pragma unroll
+      for (int u = 0; u < VW; ++u) xv[u] += rv[u];
+    }
 #pragma unroll
     for (int u = 0; u < VW; ++u) g[u] = 1.f;
     if (p.gate) ld<VW>(p.gate + (long)p.dHW.div((uint32_t)r) * p.C + c0, g);
@@ -297,6 +309,9 @@ struct BwdApplyParams {
   float* dx;
   int acc;
   FastDiv dCV;
+  const float* res;
+  float* dres;  // receives dz = d(act input), the residual branch's gradient (or NULL)
+  int dres_acc;
 };
 
 template <int VW>
@@ -323,14 +338,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
       if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
       if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
     }
-    float o[VW];
+    float rv[VW];
+#pragma unroll
+    for (int u = 0; u < VW; ++u) rv[u] = 0.f;
+    if (p.res) ld<VW>(p.res + e * VW, rv);
+    float o[VW], dzs[VW];
 #pragma unroll
     for (int u = 0; u < VW; ++u) {
       const float xh = (xv[u] - mu[u]) * is[u];
-      const float z = xh * ga[u] + be[u];
+      const float z = (xh * ga[u] + be[u]) + rv[u];
       const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
+      dzs[u] = dz;
       o[u] = (is[u] * ga[u]) * (dz - k1[u] - xh * k2[u]);
     }
+    if (p.dres) {
+#pragma unroll
+      for (int u = 0; u < VW; ++u) {
+        float* d = p.dres + e * VW + u;
+        *d = p.dres_acc ? *d + dzs[u] : dzs[u];
+      }
+    }
+    if (!p.dx) continue;
     if constexpr (VW == 4) {
       float4* d = reinterpret_cast<float4*>(p.dx + e * 4);
       float4 v = make_float4(o[0], o[1], o[2], o[3]);
@@ -423,11 +451,12 @@ extern "C" int pld_bn_stats(const float* x, int64_t rows, int c, float eps, floa
   return check_launch("stats_finalize_kernel");
 }
 
-extern "C" int pld_bn_apply(const float* x, int64_t rows, int c, const float* mean,
-                            const float* invstd, const float* gamma, const float* beta, int act,
-                            const float* gate, int hw, float* y, void* stream) {
+static int bn_apply_impl(const float* x, int64_t rows, int c, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, int act,
+                         const float* gate, int hw, const float* res, float* y, void* stream) {
   PLD_CHECK_ARG(x && y && mean && invstd && gamma && beta && rows > 0 && c > 0,
                 "pld_bn_apply: bad args");
+  PLD_CHECK_ARG(!res || c % 4 != 0 || aligned16(res), "pld_bn_add_apply: res misaligned");
   PLD_CHECK_ARG(!gate || hw > 0, "pld_bn_apply: gate needs hw > 0");
   ApplyParams p{};
   p.x = x;
@@ -439,6 +468,7 @@ extern "C" int pld_bn_apply(const float* x, int64_t rows, int c, const float* me
   p.beta = beta;
   p.act = act;
   p.gate = gate;
+  p.res = res;
   p.dHW = FastDiv((uint32_t)std::max(hw, 1));
   p.y = y;
   p.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
@@ -450,6 +480,19 @@ extern "C" int pld_bn_apply(const float* x, int64_t rows, int c, const float* me
     bn_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(p);
   }
   return check_launch("bn_apply_kernel");
+}
+
+extern "C" int pld_bn_apply(const float* x, int64_t rows, int c, const float* mean,
+                            const float* invstd, const float* gamma, const float* beta, int act,
+                            const float* gate, int hw, float* y, void* stream) {
+  return bn_apply_impl(x, rows, c, mean, invstd, gamma, beta, act, gate, hw, nullptr, y, stream);
+}
+
+extern "C" int pld_bn_add_apply(const float* x, int64_t rows, int c, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta,
+                                const float* res, int act, float* y, void* stream) {
+  PLD_CHECK_ARG(res, "pld_bn_add_apply: res is NULL");
+  return bn_apply_impl(x, rows, c, mean, invstd, gamma, beta, act, nullptr, 0, res, y, stream);
 }
 
 extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
@@ -475,11 +518,12 @@ extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const
   return check_launch("bn_apply_kernel(affine)");
 }
 
-extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
-                          const float* invstd, const float* gamma, const float* beta, int act,
-                          const float* gate, const float* addn, int hw, float* dx,
-                          int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate,
-                          void* ws, void* stream) {
+static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                       const float* invstd, const float* gamma, const float* beta, int act,
+                       const float* gate, const float* addn, int hw, const float* res,
+                       float* dx, int dx_accumulate, float* dres, int dres_accumulate,
+                       float* dgamma, float* dbeta, int param_accumulate, void* ws,
+                       void* stream) {
   PLD_CHECK_ARG(x && dy && mean && invstd && gamma && beta && ws && rows > 0 && c > 0,
                 "pld_bn_bwd: bad args");
   PLD_CHECK_ARG(rows < (1L << 31), "pld_bn_bwd: too many rows");
@@ -497,6 +541,7 @@ extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, 
   p.act = act;
   p.gate = gate;
   p.addn = addn;
+  p.res = res;
   p.dHW = FastDiv((uint32_t)std::max(hw, 1));
   p.partial = (double*)ws;
   int rc = launch_reduce(RED_BNBWD, p, st);
@@ -507,7 +552,7 @@ extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, 
   bnbwd_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
                                                        param_accumulate, k12);
   rc = check_launch("bnbwd_finalize_kernel");
-  if (rc || !dx) return rc;
+  if (rc || !(dx || dres)) return rc;
   BwdApplyParams q{};
   q.x = x;
   q.dy = dy;
@@ -525,10 +570,35 @@ extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, 
   q.dx = dx;
   q.acc = dx_accumulate;
   q.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
+  q.res = res;
+  q.dres = dres;
+  q.dres_acc = dres_accumulate;
   if (c % 4 == 0) {
     bn_bwd_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(q);
   } else {
     bn_bwd_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(q);
   }
   return check_launch("bn_bwd_apply_kernel");
+}
+
+extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, int act,
+                          const float* gate, const float* addn, int hw, float* dx,
+                          int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate,
+                          void* ws, void* stream) {
+  return bn_bwd_impl(x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn, hw, nullptr,
+                     dx, dx_accumulate, nullptr, 0, dgamma, dbeta, param_accumulate, ws, stream);
+}
+
+extern "C" int pld_bn_add_bwd(const float* x, const float* dy, int64_t rows, int c,
+                              const float* mean, const float* invstd, const float* gamma,
+                              const float* beta, const float* res, int act, float* dx,
+                              int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
+                              float* dbeta, int param_accumulate, void* ws, void* stream) {
+  PLD_CHECK_ARG(res, "pld_bn_add_bwd: res is NULL");
+  PLD_CHECK_ARG(c % 4 != 0 || ((aligned16(res)) && (!dres || aligned16(dres))),
+                "pld_bn_add_bwd: res/dres misaligned");
+  return bn_bwd_impl(x, dy, rows, c, mean, invstd, gamma, beta, act, nullptr, nullptr, 0, res,
+                     dx, dx_accumulate, dres, dres_accumulate, dgamma, dbeta, param_accumulate,
+                     ws, stream);
 }

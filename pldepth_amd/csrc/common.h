@@ -32,6 +32,7 @@ int check_launch(const char* what);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // ---- activations (Keras semantics) ----
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };

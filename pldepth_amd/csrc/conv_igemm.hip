@@ -458,6 +458,37 @@ __global__ __launch_bounds__(256) void splitk_out_kernel(const float* __restrict
   }
 }
 
+// strided 1x1 dgrad: dx[img][y][x][c] = (y%sh==0 && x%sw==0) ? t[img][y/sh][x/sw][c] : 0, with
+// the channel range split across two destinations (concat inputs)
+__global__ __launch_bounds__(256) void stride_scatter_kernel(const float* __restrict__ t, int n,
+                                                             int h, int w, int oh, int ow,
+                                                             int sh, int sw, int C,
+                                                             float* out1, int c1, int acc1,
+                                                             float* out2, int acc2) {
+  const long total = (long)n * h * w * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long pix = i / C;
+    const int x = (int)(pix % w);
+    pix /= w;
+    const int y = (int)(pix % h);
+    const long img = pix / h;
+    float v = 0.f;
+    if (y % sh == 0 && x % sw == 0 && y / sh < oh && x / sw < ow)
+      v = t[((img * oh + y / sh) * ow + x / sw) * C + c];
+    const long px = (img * h + y) * w + x;
+    if (c < c1) {
+      float* d = out1 + px * c1 + c;
+      *d = acc1 ? *d + v : v;
+    } else {
+      const int c2 = C - c1;
+      float* d = out2 + px * c2 + (c - c1);
+      *d = acc2 ? *d + v : v;
+    }
+  }
+}
+
 // HWIO [kh][kw][ci][co] -> [co][kh][kw][ci]
 __global__ void filter_native_kernel(const float* __restrict__ w, int taps, int cin, int cout,
                                      float* __restrict__ o) {
@@ -576,7 +607,6 @@ static int fill_geom(const pld_conv_args* a, GemmConvParams& p) {
   return PLD_OK;
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace pld
 
@@ -695,9 +725,16 @@ extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
                       (long)a->kh * a->kw * (a->c1 + a->c2), a->tile);
 }
 
+static size_t strided_tmp_bytes(const pld_conv_args* a) {
+  return ((sizeof(float) * (size_t)a->n * a->oh * a->ow * (a->c1 + a->c2)) + 255) / 256 * 256;
+}
+
 extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->h <= 0 || a->w <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;
+  if (a->sh != 1 || a->sw != 1)  // 1x1 strided: GEMM into a compact tmp, then scatter
+    return strided_tmp_bytes(a) + fwd_ws_bytes((long)a->n * a->oh * a->ow, a->c1 + a->c2,
+                                               a->cout, a->tile);
   return fwd_ws_bytes((long)a->n * a->h * a->w, a->c1 + a->c2, (long)a->kh * a->kw * a->cout,
                       a->tile);
 }
@@ -706,10 +743,60 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
                                 float* dx1, int accumulate1, float* dx2, int accumulate2,
                                 void* stream) {
   PLD_CHECK_ARG(a && dy && w_dgrad && dx1, "pld_conv2d_dgrad: null pointer");
-  PLD_CHECK_ARG(a->sh == 1 && a->sw == 1, "pld_conv2d_dgrad: only stride 1 is supported");
   PLD_CHECK_ARG(a->c2 == 0 || dx2, "pld_conv2d_dgrad: dx2 required for a two-source conv");
   PLD_CHECK_ARG(a->in_scale == nullptr,
                 "pld_conv2d_dgrad: the input prologue's gradient is the caller's (pass NULL)");
+  if (a->sh != 1 || a->sw != 1) {
+    // ResNet projection / downsampling convs (1x1, stride s, no padding): a plain GEMM
+    // t[img][oy][ox][:] = dy[img][oy][ox][:] . W^T, scattered to the stride grid
+    PLD_CHECK_ARG(a->kh == 1 && a->kw == 1 && a->pad_t == 0 && a->pad_l == 0 && a->sh > 0 &&
+                      a->sw > 0,
+                  "pld_conv2d_dgrad: strided dgrad is implemented for 1x1 unpadded convs only");
+    PLD_CHECK_ARG(a->n > 0 && a->oh > 0 && a->ow > 0 && a->h > 0 && a->w > 0 && a->cout > 0,
+                  "pld_conv2d_dgrad: bad geometry");
+    const size_t tb = strided_tmp_bytes(a);
+    const size_t need = pld_conv2d_dgrad_workspace_size(a);
+    PLD_CHECK_ARG(a->ws && a->ws_bytes >= need, "pld_conv2d_dgrad: strided workspace %zu < %zu",
+                  a->ws_bytes, need);
+    const int C = a->c1 + a->c2;
+    pld_conv_args g = *a;
+    g.x1 = dy;
+    g.x2 = nullptr;
+    g.c1 = a->cout;
+    g.c2 = 0;
+    g.h = g.oh = a->oh;
+    g.w = g.ow = a->ow;
+    g.sh = g.sw = 1;
+    g.cout = C;
+    g.in_scale = g.in_shift = nullptr;
+    GemmConvParams p;
+    int rc = fill_geom(&g, p);
+    if (rc) return rc;
+    float* t = (float*)a->ws;
+    p.bmat = w_dgrad;
+    p.M = (long)a->n * a->oh * a->ow;
+    p.N = C;
+    p.K = a->cout;
+    p.bias = nullptr;
+    p.out1 = t;
+    p.ld1 = C;
+    p.acc1 = 0;
+    p.out2 = nullptr;
+    p.ld2 = 0;
+    p.acc2 = 0;
+    p.split = C;
+    const bool vec = (p.c1 % 4 == 0) && aligned16(dy) && aligned16(w_dgrad);
+    const bool vec16 = vec && (p.c1 % 16 == 0);
+    hipStream_t st = as_stream(stream);
+    rc = run_fwd_gemm(p, vec, vec16, a->tile, (char*)a->ws + tb, a->ws_bytes - tb, st,
+                      "pld_conv2d_dgrad");
+    if (rc) return rc;
+    const long total = (long)a->n * a->h * a->w * C;
+    stride_scatter_kernel<<<std::min<unsigned>(cdiv(total, 256), 16384), 256, 0, st>>>(
+        t, a->n, a->h, a->w, a->oh, a->ow, a->sh, a->sw, C, dx1, a->c1, accumulate1, dx2,
+        accumulate2);
+    return check_launch("stride_scatter_kernel");
+  }
   if (pld__skinny_eligible(a) && aligned16(dx1))
     return pld__skinny_dgrad(a, dy, w_dgrad, dx1, accumulate1, stream);
   // dx[img][iy][ix][ci] = sum_{ty,tx,co} dy[img][iy+ty-pt'][ix+tx-pl'][co] * Wd[ci][ty][tx][co]

@@ -294,6 +294,36 @@ def bn_bwd(x, dy, rows, c, mean, invstd, gamma, beta, act, dx, dgamma, dbeta, ga
                      ptr(dgamma), ptr(dbeta), int(param_accumulate), ptr(ws), stream())
 
 
+def bn_add_apply(x, rows, c, mean, invstd, gamma, beta, res, act, y):
+    lib().pld_bn_add_apply(ptr(x), rows, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                           ptr(res), ACT[act], ptr(y), stream())
+
+
+def bn_add_bwd(x, dy, rows, c, mean, invstd, gamma, beta, res, act, dx, dres, dgamma, dbeta,
+               dx_accumulate=False, dres_accumulate=False, param_accumulate=False):
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_bn_add_bwd(ptr(x), ptr(dy), rows, c, ptr(mean), ptr(invstd), ptr(gamma),
+                         ptr(beta), ptr(res), ACT[act], ptr(dx), int(dx_accumulate), ptr(dres),
+                         int(dres_accumulate), ptr(dgamma), ptr(dbeta), int(param_accumulate),
+                         ptr(ws), stream())
+
+
+def maxpool2d_fwd(x, k, s, pad_t, pad_l, y, argmax=None):
+    n, h, w, c = x.shape
+    oh, ow = y.shape[1], y.shape[2]
+    lib().pld_maxpool2d_fwd(ptr(x), n, h, w, c, k, s, pad_t, pad_l, oh, ow, ptr(y), ptr(argmax),
+                            stream())
+    return y
+
+
+def maxpool2d_bwd(dy, argmax, k, s, pad_t, pad_l, dx, accumulate=False):
+    n, h, w, c = dx.shape
+    oh, ow = dy.shape[1], dy.shape[2]
+    lib().pld_maxpool2d_bwd(ptr(dy), ptr(argmax), n, h, w, c, k, s, pad_t, pad_l, oh, ow, ptr(dx),
+                            int(accumulate), stream())
+    return dx
+
+
 def channel_affine_act(x, rows, c, scale, shift, act, y):
     lib().pld_channel_affine_act(ptr(x), rows, c, ptr(scale), ptr(shift), ACT[act], ptr(y),
                                  stream())

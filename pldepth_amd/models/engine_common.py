@@ -1,0 +1,145 @@
+"""Building blocks shared by the HIP model engines (ff_effnet, ff_redweb): flat parameter
+stores and Keras-named BatchNormalization / Conv2D wrappers around libpldepth_hip.so."""
+import numpy as np
+import torch
+
+from .. import kernels as K
+
+BN_EPS = 1e-3        # keras BatchNormalization defaults
+BN_MOMENTUM = 0.99
+
+
+class FlatStore:
+    """Named views into one flat fp32 device buffer (16-byte aligned segments)."""
+
+    def __init__(self):
+        self.specs = []  # (name, shape, offset)
+        self.size = 0
+        self.buf = None
+        self.views = {}
+
+    def add(self, name, shape):
+        n = int(np.prod(shape))
+        self.specs.append((name, tuple(shape), self.size))
+        self.size += (n + 3) // 4 * 4
+        return name
+
+    def materialize(self, device):
+        self.buf = torch.zeros(max(self.size, 4), dtype=torch.float32, device=device)
+        for name, shape, off in self.specs:
+            n = int(np.prod(shape))
+            self.views[name] = self.buf[off:off + n].view(shape)
+        return self
+
+    def like(self):
+        t = FlatStore()
+        t.specs, t.size = self.specs, self.size
+        return t
+
+    def __getitem__(self, name):
+        return self.views[name]
+
+    def names(self):
+        return [s[0] for s in self.specs]
+
+
+class _BN:
+    """One Keras BatchNormalization (training mode: batch statistics + moving-average update;
+    inference: moving statistics)."""
+
+    def __init__(self, eng, name, c, eps=BN_EPS, momentum=BN_MOMENTUM):
+        self.name, self.c = name, c
+        self.eps, self.momentum = eps, momentum
+        self.g = eng.params.add(name + "/gamma", (c,))
+        self.b = eng.params.add(name + "/beta", (c,))
+        self.mm = eng.stats.add(name + "/moving_mean", (c,))
+        self.mv = eng.stats.add(name + "/moving_variance", (c,))
+        eng.bns.append(self)
+
+    def bind(self, eng):
+        dev = eng.device
+        self.gamma, self.beta = eng.params[self.g], eng.params[self.b]
+        self.dgamma, self.dbeta = eng.grads[self.g], eng.grads[self.b]
+        self.mmean, self.mvar = eng.stats[self.mm], eng.stats[self.mv]
+        self.mean = torch.empty(self.c, device=dev)
+        self.invstd = torch.empty(self.c, device=dev)
+        self.inf_scale = torch.empty(self.c, device=dev)
+        self.inf_shift = torch.empty(self.c, device=dev)
+
+    def stats_(self, x, rows, training):
+        if training:
+            K.bn_stats(x, rows, self.c, self.mean, self.invstd, self.mmean, self.mvar, self.eps,
+                       self.momentum)
+        else:
+            K.bn_inference_coeffs(self.gamma, self.beta, self.mmean, self.mvar, self.inf_scale,
+                                  self.inf_shift, self.eps)
+
+    def apply(self, x, rows, act, y, training, gate=None, hw=0):
+        if training:
+            K.bn_apply(x, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, act, y,
+                       gate=gate, hw=hw)
+        else:
+            assert gate is None
+            K.channel_affine_act(x, rows, self.c, self.inf_scale, self.inf_shift, act, y)
+
+    def bwd(self, x, dy, rows, act, dx, dx_acc=False, gate=None, addn=None, hw=0):
+        K.bn_bwd(x, dy, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, act, dx,
+                 self.dgamma, self.dbeta, gate=gate, addn=addn, hw=hw, dx_accumulate=dx_acc)
+
+    def add_apply(self, x, rows, res, act, y, training):
+        """y = act(bn(x) + res)"""
+        if training:
+            K.bn_add_apply(x, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, res,
+                           act, y)
+        else:
+            if act == "none":
+                K.channel_affine_act(x, rows, self.c, self.inf_scale, self.inf_shift, "none", y)
+                K.residual_add(y, None, res, y)
+            else:  # identity statistics turn bn_add_apply into act(z + res)
+                K.channel_affine_act(x, rows, self.c, self.inf_scale, self.inf_shift, "none", y)
+                z, o = _ident(self.c, x.device)
+                K.bn_add_apply(y, rows, self.c, z, o, o, z, res, act, y)
+
+    def add_bwd(self, x, dy, rows, res, act, dx, dres, dx_acc=False, dres_acc=False):
+        K.bn_add_bwd(x, dy, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, res, act,
+                     dx, dres, self.dgamma, self.dbeta, dx_accumulate=dx_acc,
+                     dres_accumulate=dres_acc)
+
+
+_IDENT = {}
+
+
+def _ident(c, device):
+    """(zeros, ones) per channel count: a BN apply with these statistics is exact identity."""
+    key = (c, str(device))
+    if key not in _IDENT:
+        _IDENT[key] = (torch.zeros(c, device=device), torch.ones(c, device=device))
+    return _IDENT[key]
+
+
+class _Conv:
+    def __init__(self, eng, name, k, cin, cout, stride=1, bias=False, trainable=False,
+                 need_dgrad=True):
+        self.name, self.k, self.cin, self.cout, self.stride = name, k, cin, cout, stride
+        self.has_bias, self.trainable, self.need_dgrad = bias, trainable, need_dgrad
+        store = eng.params if trainable else eng.frozen
+        self.wk = store.add(name + "/kernel", (k, k, cin, cout))
+        self.bk = store.add(name + "/bias", (cout,)) if bias else None
+        eng.convs.append(self)
+
+    def bind(self, eng):
+        store = eng.params if self.trainable else eng.frozen
+        self.w = store[self.wk]
+        self.b = store[self.bk] if self.bk else None
+        if self.trainable:
+            self.dw = eng.grads[self.wk]
+            self.db = eng.grads[self.bk] if self.bk else None
+        dev = eng.device
+        self.w_nat = torch.empty(self.cout, self.k, self.k, self.cin, device=dev)
+        self.w_dg = (torch.empty(self.cin, self.k, self.k, self.cout, device=dev)
+                     if self.need_dgrad else None)
+
+    def refresh(self):
+        K.filter_to_native(self.w, self.w_nat)
+        if self.w_dg is not None:
+            K.filter_to_dgrad(self.w, self.w_dg)

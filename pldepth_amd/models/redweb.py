@@ -1,26 +1,24 @@
 """ff_redweb (ResNet-50 encoder + ReDWeb feature-fusion decoder; pldepth/models/redweb.py:402-434).
 
-The ResNet-50/ReDWeb HIP engine is not built yet (BASELINE cfg3): this
-surface exists so callers get a clear error instead of an import failure. ``preprocess_input``
-is Keras' caffe-mode ResNet50 preprocessing (RGB->BGR, minus ImageNet means), applied as the
-reference does to [0,1] inputs.
+``ReDWebNetTFVersion.get_model_and_normalization(input_shape, ranking_size, loss_type)`` returns
+``(model, preprocess_fn)`` like the reference: the model is a FullyFledgedModel over the HIP
+engine ``RedWebFF`` (pldepth_amd/models/redweb_ff.py); ``preprocess_fn`` is Keras' caffe-mode
+ResNet50 preprocessing (RGB->BGR, minus ImageNet means), which the reference's pipeline applies
+to its [0,1] images (PLDepth.py:169-173) — callers apply it, the model does not.
 """
-import numpy as np
-
 from ..losses.losses_meta import DepthLossType
 from .pl_hourglass import FullyFledgedModel
+from .redweb_ff import CAFFE_MEAN_BGR, preprocess_input  # noqa: F401
 
-CAFFE_MEAN_BGR = np.array([103.939, 116.779, 123.68], np.float32)
-
-
-def preprocess_input_resnet(x, data_format=None):
-    x = np.asarray(x, np.float32)[..., ::-1]
-    return x - CAFFE_MEAN_BGR
+preprocess_input_resnet = preprocess_input
 
 
 class ReDWebNetTFVersion(FullyFledgedModel):
     @staticmethod
     def get_model_and_normalization(input_shape, ranking_size, loss_type=DepthLossType.NLL,
                                     batch_size=4, seed=0):
-        raise NotImplementedError(
-            "ff_redweb (ResNet-50 + ReDWeb decoder) has no HIP engine yet; use ff_effnet")
+        from .redweb_ff import RedWebFF
+        if loss_type != DepthLossType.NLL:
+            raise ValueError(f"unsupported loss type {loss_type}")
+        eng = RedWebFF(tuple(input_shape), batch_size, seed=seed)
+        return ReDWebNetTFVersion(eng, batch_size=batch_size), preprocess_input

@@ -17,6 +17,9 @@ import torch
 
 from . import kernels as K
 from .models.effnet_ff import EffNetFF
+from .models.redweb_ff import RedWebFF
+
+ENGINES = {"ff_effnet": EffNetFF, "ff_redweb": RedWebFF, "ff_resnet": RedWebFF}
 
 SAMPLING_TYPES = {0: "thresh", 1: "info", 3: "pure"}  # PLDepth.py:97-108 --sampling_type
 
@@ -28,8 +31,8 @@ class ReplicaTrainer:
                  gpu_sampler=True, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
         """gpu_sampler=False: rankings come from the caller (set_rankings), as model.fit feeds
         y_true batches; otherwise the GPU sampler draws them from (gt, mask) each step."""
-        if model != "ff_effnet" and engine is None:
-            raise NotImplementedError(f"model {model!r}: only ff_effnet has a HIP engine yet")
+        if engine is None and model not in ENGINES:
+            raise ValueError(f"unknown model {model!r} (expected one of {sorted(ENGINES)})")
         self.gpu_sampler = gpu_sampler
         self.betas = (beta_1, beta_2, epsilon)
         self.B, self.L, self.R = batch_size, ranking_size, rankings_per_image
@@ -41,8 +44,8 @@ class ReplicaTrainer:
         self.seed = seed
         dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        self.engine = engine if engine is not None else EffNetFF(input_shape, batch_size,
-                                                                 device=dev, seed=seed)
+        self.engine = engine if engine is not None else ENGINES[model](input_shape, batch_size,
+                                                                       device=dev, seed=seed)
         self.engine.drop_connect = drop_connect
         B, H, W, L, R = self.B, self.H, self.W, self.L, self.R
         self.n_cand = K.sampler_candidates(R, self.strategy)
@@ -70,7 +73,9 @@ class ReplicaTrainer:
 
     # ------------------------------------------------------------------ data
     def set_batch(self, images, gt, mask):
-        """images [B,H,W,3] in [0,1], gt [B,H,W], mask [B,H,W] (>0 valid) — host or device.
+        """images [B,H,W,3] model input (the [0,1] images after the model's preprocess_fn:
+        identity for ff_effnet, caffe mean subtraction for ff_redweb), gt [B,H,W], mask [B,H,W]
+        (>0 valid) — host or device.
         The copies are ordered on the trainer's stream (before the next step's kernels)."""
         with torch.cuda.stream(self.stream):
             if images is not None:

@@ -104,6 +104,23 @@ def test_fit_predict_save_load(cuda, tmp_path):
     np.testing.assert_array_equal(model2.predict(imgs[:3]), p1)
 
 
-def test_redweb_reports_unbuilt(cuda):
-    with pytest.raises(NotImplementedError):
-        get_pl_depth_net(_params(model="ff_redweb"), [64, 64, 3])
+def test_redweb_factory_fit_predict(cuda):
+    """ff_redweb through the reference's factory: (model, caffe preprocess_fn), compile, fit."""
+    B, H, L, R = 2, 64, 5, 20
+    mp = _params(B, L, R, model="ff_redweb")
+    mp.set_parameter("sampling_strategy", InformationScoreBasedSampling(mp))
+    model, pre = get_pl_depth_net(mp, [H, H, 3])
+    imgs, gts, masks = synthetic_hrwsi(4, H, H, seed=1)
+    x = pre(imgs)
+    assert np.allclose(x[..., 0], imgs[..., 2] - 103.939, atol=1e-4)  # BGR, caffe means
+    model.compile(loss=HourglassNegativeLogLikelihood(L, B), optimizer=Adam(0.01, amsgrad=True))
+    prov = HourglassLargeScaleDataProvider(mp, masks, masks[:2], augmentation=False)
+    w0 = model.get_weights()
+    model.fit(x=prov.provide_train_dataset(x, gts), epochs=1, steps_per_epoch=2, verbose=0)
+    w1 = model.get_weights()
+    assert np.isfinite(model.history["loss"]).all()
+    assert not np.allclose(w0["ffl0/conv0/kernel"], w1["ffl0/conv0/kernel"])
+    np.testing.assert_array_equal(w0["conv3_block2_2_conv/kernel"],
+                                  w1["conv3_block2_2_conv/kernel"])  # encoder convs frozen
+    assert not np.allclose(w0["conv3_block2_2_bn/gamma"], w1["conv3_block2_2_bn/gamma"])
+    assert model.predict(x[:3]).shape == (3, H, H, 1)

@@ -427,3 +427,113 @@ def test_sampler_draws_uniform_and_in_range(cuda):
     e = torch.empty(2, n_cand, L, dtype=torch.int32, device=cuda)
     K.sampler_draw(nv[2:].contiguous(), n_cand, L, seed=1234, step=7, image_offset=2, draws=e)
     assert torch.equal(e.cpu(), d[2:])
+
+
+# ------------------------------------------------------------------- ResNet / ReDWeb pieces
+@pytest.mark.parametrize("case", [(2, 8, 8, 64, 256, 2), (1, 14, 10, 256, 128, 2),
+                                  (2, 7, 9, 32, 20, 2), (1, 6, 6, 16, 64, 3)])
+def test_strided_1x1_conv_fwd_dgrad_wgrad(cuda, case):
+    """ResNet-50 downsampling / projection convs: 1x1, stride s, no padding (keras resnet
+    block1 `_0_conv` / `_1_conv`), including odd sizes where the last row/col is skipped."""
+    n, h, w, cin, cout, s = case
+    torch.manual_seed(11)
+    x = torch.randn(n, h, w, cin, dtype=torch.float64)
+    wt = torch.randn(1, 1, cin, cout, dtype=torch.float64) / np.sqrt(cin)
+    b = torch.randn(cout, dtype=torch.float64)
+    xr, wr = x.clone().requires_grad_(True), wt.clone().requires_grad_(True)
+    y_ref = OE.conv(xr.permute(0, 3, 1, 2), wr, b, s).permute(0, 2, 3, 1)
+    oh, ow = y_ref.shape[1], y_ref.shape[2]
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    gx, gw = dev(x, cuda), dev(wt, cuda)
+    args = K.conv_args(gx, None, 1, 1, s, 0, 0, oh, ow, cout)
+    y = torch.empty(n, oh, ow, cout, device=cuda)
+    K.conv2d_fwd(args, K.filter_to_native(gw), dev(b, cuda), y)
+    gdy = dev(dy, cuda)
+    dw = torch.empty(1, 1, cin, cout, device=cuda)
+    K.conv2d_wgrad(args, gdy, dw)
+    dx = torch.full_like(gx, 3.0)
+    K.conv2d_dgrad(args, gdy, K.filter_to_dgrad(gw), dx, acc1=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+    assert rel_err(dw, wr.grad) < 1e-5
+    assert rel_err(dx - 3.0, xr.grad) < 1e-5
+    dx2 = torch.empty_like(gx)
+    K.conv2d_dgrad(args, gdy, K.filter_to_dgrad(gw), dx2)
+    torch.cuda.synchronize()
+    assert rel_err(dx2, xr.grad) < 1e-5
+
+
+def test_resnet_stem_conv(cuda):
+    """ZeroPadding2D(3) + Conv2D(64, 7, strides=2) (+bias) on a 3-channel image."""
+    n, h, w = 2, 32, 40
+    torch.manual_seed(12)
+    x = torch.randn(n, h, w, 3, dtype=torch.float64) * 50
+    wt = torch.randn(7, 7, 3, 64, dtype=torch.float64) * 0.05
+    b = torch.randn(64, dtype=torch.float64)
+    y_ref = OE.conv(x.permute(0, 3, 1, 2), wt, b, 2, (3, 3, 3, 3)).permute(0, 2, 3, 1)
+    oh, ow = y_ref.shape[1:3]
+    assert (oh, ow) == (h // 2, w // 2)
+    args = K.conv_args(dev(x, cuda), None, 7, 7, 2, 3, 3, oh, ow, 64)
+    y = torch.empty(n, oh, ow, 64, device=cuda)
+    K.conv2d_fwd(args, K.filter_to_native(dev(wt, cuda)), dev(b, cuda), y)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+
+
+@pytest.mark.parametrize("shape,relu", [((2, 16, 20, 64), True), ((1, 9, 7, 12), False),
+                                        ((2, 15, 15, 5), True)])
+def test_maxpool_zero_padded(cuda, shape, relu):
+    from oracle import redweb as OR
+    torch.manual_seed(13)
+    x = torch.randn(*shape, dtype=torch.float64).float().double()  # fp32-exact: same order
+    if relu:
+        x = torch.relu(x)  # zeros tie with the padding, as after conv1_relu
+    xr = x.clone().requires_grad_(True)
+    y_ref = OR.maxpool_zero_padded(xr.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    n, h, w, c = shape
+    oh, ow = y_ref.shape[1:3]
+    y = torch.empty(n, oh, ow, c, device=cuda)
+    am = torch.empty(n, oh, ow, c, dtype=torch.uint8, device=cuda)
+    K.maxpool2d_fwd(dev(x, cuda), 3, 2, 1, 1, y, am)
+    dx = torch.empty(n, h, w, c, device=cuda)
+    K.maxpool2d_bwd(dev(dy, cuda), am, 3, 2, 1, 1, dx)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) == 0.0
+    assert rel_err(dx, xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("rows,c,act", [(3000, 64, "relu"), (517, 256, "none"),
+                                        (200, 6, "relu")])
+def test_bn_add_forward_backward(cuda, rows, c, act):
+    from oracle import redweb as OR
+    torch.manual_seed(rows + c)
+    x = torch.randn(rows, c, dtype=torch.float64) * 2 + 0.5
+    res = torch.randn(rows, c, dtype=torch.float64)
+    gamma = torch.rand(c, dtype=torch.float64) + 0.5
+    beta = torch.randn(c, dtype=torch.float64)
+    xr, rr, gr, br = (t.clone().requires_grad_(True) for t in (x, res, gamma, beta))
+    z = OR.bn_train(xr.T.reshape(1, c, rows, 1), gr, br, OR.RESNET_BN_EPS)
+    z = z.reshape(c, rows).T + rr
+    y_ref = torch.relu(z) if act == "relu" else z
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    gx = dev(x, cuda)
+    gm, gi = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_stats(gx, rows, c, gm, gi, None, None, OR.RESNET_BN_EPS)
+    y = torch.empty_like(gx)
+    gres, ggam, gbet = dev(res, cuda), dev(gamma, cuda), dev(beta, cuda)
+    K.bn_add_apply(gx, rows, c, gm, gi, ggam, gbet, gres, act, y)
+    dx = torch.empty_like(gx)
+    dres = torch.full_like(gx, 2.0)
+    dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_add_bwd(gx, dev(dy, cuda), rows, c, gm, gi, ggam, gbet, gres, act, dx, dres, dg, db,
+                 dres_accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+    assert rel_err(dx, xr.grad) < 1e-4
+    assert rel_err(dres - 2.0, rr.grad) < 1e-5
+    assert rel_err(dg, gr.grad) < 1e-5
+    assert rel_err(db, br.grad) < 1e-5

@@ -150,3 +150,28 @@ def test_hourglass_loss_gather_and_scatter():
         pp[b, p] -= 2 * eps
         lm, _ = LM.hourglass_nll(y, pp.reshape(pred.shape), B, L)
         assert abs((lp - lm) / (2 * eps) - dpred.reshape(B, -1)[b, p]) < 1e-7
+
+
+def test_redweb_oracle_counts_match_survey():
+    """142.54 GFLOP per 448x448 image per train step, 53,120
+    encoder-BN parameters, ~8.65 M trainable in total."""
+    from oracle import redweb as OR
+    assert abs(OR.conv_flops_per_image(448, 448) / 1e9 - 142.54) < 0.01
+    spec = OR.param_specs()
+    enc_bn = sum(int(np.prod(s)) for n, s, k in spec
+                 if k == "trainable" and not n.startswith(("ffl", "aol")))
+    assert enc_bn == 53120
+    assert sum(int(np.prod(s)) for n, s, k in spec if k == "trainable") == 8647299
+
+
+def test_redweb_oracle_shapes_small():
+    from oracle import redweb as OR
+    torch.manual_seed(0)
+    P = {n: torch.randn(s, dtype=torch.float64) * 0.05 for n, s, _ in OR.param_specs()}
+    taps = {}
+    with torch.no_grad():
+        out = OR.forward(P, torch.rand(1, 64, 64, 3, dtype=torch.float64), taps=taps)
+    assert out.shape == (1, 64, 64, 1)
+    assert taps["conv2_block3_out"].shape == (1, 256, 16, 16)
+    assert taps["conv5_block3_out"].shape == (1, 2048, 2, 2)
+    assert taps["ffl2"].shape == (1, 64, 32, 32)
