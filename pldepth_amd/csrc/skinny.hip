@@ -1,5 +1,6 @@
-// 3x3 'same' convolutions with ONE output channel (the decoder's final Conv2D(1, 3x3),
-// pldepth/models/pl_hourglass.py:96) as direct, LDS-tiled, HBM-bound kernels.
+// 3x3 'same' convolutions with ONE output channel (the ff_effnet decoder's final Conv2D(1, 3x3),
+// pldepth/models/pl_hourglass.py:96; ReDWeb's AdaptiveOutputLayer conv1, redweb.py:322) as
+// direct, LDS-tiled, HBM-bound kernels.
 //
 // An implicit GEMM with N = 1 wastes 31/32 of every 32x32 MFMA tile; the layer's arithmetic
 // (288 MACs per output pixel) is far below the HBM roofline, so each kernel instead streams its
@@ -128,41 +129,54 @@ __global__ __launch_bounds__(256) void skinny_dgrad_kernel(SkinnyParams p) {
 // 576 threads = 2 pixel halves x 288 (tap, channel) pairs: every thread does equal work
 constexpr int WG_THREADS = 576;
 
+constexpr int MAX_C = 2 * CH;  // eligibility bound (ReDWeb's aol/conv1 has 64 input channels)
+
 __global__ __launch_bounds__(WG_THREADS) void skinny_wgrad_kernel(SkinnyParams p) {
   __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
   __shared__ float dyl[ST * ST];
-  __shared__ float comb[9 * CH];
+  __shared__ float comb[9 * MAX_C];
   const int ntiles = p.tiles_x * p.tiles_y * p.n;
-  const int nE = 9 * p.c;  // c <= CH (eligibility)
   const int half = threadIdx.x / (9 * CH);
   const int e = threadIdx.x % (9 * CH);
-  const int t = e / p.c, cc = e % p.c;
-  const bool act = e < nE;
-  float acc = 0.f;
+  const int nchunks = (p.c + CH - 1) / CH;
+  float acc[MAX_C / CH] = {0.f, 0.f};
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int img = tile / (p.tiles_x * p.tiles_y);
     const int r = tile % (p.tiles_x * p.tiles_y);
     const int y0 = (r / p.tiles_x) * ST, x0 = (r % p.tiles_x) * ST;
     __syncthreads();
-    stage_halo(p, halo, img, y0, x0, 0, p.c);
     if (threadIdx.x < ST * ST) {
       const int oy = y0 + threadIdx.x / ST, ox = x0 + threadIdx.x % ST;
       dyl[threadIdx.x] = (oy < p.h && ox < p.w) ? p.dy[((long)img * p.h + oy) * p.w + ox] : 0.f;
     }
-    __syncthreads();
-    if (act) {
-      const float* hp = halo + ((t / 3) * HT + t % 3) * CS + cc;
-      float s = 0.f;
-      for (int py = half * (ST / 2); py < (half + 1) * (ST / 2); ++py)
+#pragma unroll
+    for (int k = 0; k < MAX_C / CH; ++k) {
+      if (k >= nchunks) break;
+      const int c0 = k * CH, nc = min(CH, p.c - c0);
+      if (k > 0) __syncthreads();
+      stage_halo(p, halo, img, y0, x0, c0, nc);
+      __syncthreads();
+      if (e < 9 * nc) {
+        const int t = e / nc, cc = e % nc;
+        const float* hp = halo + ((t / 3) * HT + t % 3) * CS + cc;
+        float s = 0.f;
+        for (int py = half * (ST / 2); py < (half + 1) * (ST / 2); ++py)
 #pragma unroll 8
-        for (int px = 0; px < ST; ++px) s += hp[(py * HT + px) * CS] * dyl[py * ST + px];
-      acc += s;
+          for (int px = 0; px < ST; ++px) s += hp[(py * HT + px) * CS] * dyl[py * ST + px];
+        acc[k] += s;
+      }
     }
   }
-  __syncthreads();
-  if (half == 1 && act) comb[e] = acc;
-  __syncthreads();
-  if (half == 0 && act) p.part[(long)blockIdx.x * nE + e] = acc + comb[e];
+  // combine the two pixel halves; partial index = tap * c + channel (HWIO with cout 1)
+  for (int k = 0; k < nchunks; ++k) {
+    const int c0 = k * CH, nc = min(CH, p.c - c0);
+    const bool act = e < 9 * nc;
+    const int o = act ? (e / nc) * p.c + c0 + e % nc : 0;
+    __syncthreads();
+    if (half == 1 && act) comb[o] = acc[k];
+    __syncthreads();
+    if (half == 0 && act) p.part[(long)blockIdx.x * 9 * p.c + o] = acc[k] + comb[o];
+  }
 }
 
 // one workgroup per output: strided partial sums then a fixed-shape tree (deterministic)
@@ -189,10 +203,10 @@ constexpr int SKINNY_WG_BLOCKS = 2048;
 
 using namespace pld;
 
-// eligibility: 3x3 stride-1 'same', single source, no prologue, cout 1, c % 4 == 0
+// eligibility: 3x3 stride-1 'same', single source, no prologue, cout 1, c % 4 == 0, c <= 64
 extern "C" int pld__skinny_eligible(const pld_conv_args* a) {
   return a && a->cout == 1 && a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 &&
-         a->c2 == 0 && a->in_scale == nullptr && a->c1 % 4 == 0 && a->c1 <= CH &&
+         a->c2 == 0 && a->in_scale == nullptr && a->c1 % 4 == 0 && a->c1 <= MAX_C &&
          a->oh == a->h && a->ow == a->w && a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 &&
          a->pad_l <= 2;
 }

@@ -130,6 +130,7 @@ def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None,
     a.in_shift = None if in_shift is None else in_shift.data_ptr()
     a.in_act = ACT[in_act]
     a.tile = -1
+    a._keep = (x1, x2, in_scale, in_shift)  # the struct holds raw pointers: keep owners alive
     return a
 
 
@@ -176,7 +177,7 @@ def _shape_key(mode, a):
 
 def _skinny(a):
     return (a.cout == 1 and a.kh == 3 and a.kw == 3 and a.sh == 1 and a.c2 == 0
-            and not a.in_scale and a.c1 % 4 == 0 and a.c1 <= 32)
+            and not a.in_scale and a.c1 % 4 == 0 and a.c1 <= 64)
 
 
 def _tune(mode, a, run):
