@@ -55,35 +55,34 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int BK = 16;
 constexpr int PADK = 4;  // [row][BK+PADK]: 80-byte rows -> conflict-free b128 fragment reads
 
-// load one element of the (prologue-transformed) activation at pixel (img, iy, ix), channel k-part
-__device__ __forceinline__ float load_x(const GemmConvParams& p, int img, int iy, int ix, int ci) {
-  if (iy < 0 || iy >= p.h || ix < 0 || ix >= p.w) return 0.f;
-  const long pix = ((long)img * p.h + iy) * p.w + ix;
-  if (ci < p.c1) {
-    float v = p.x1[pix * p.c1 + ci];
-    if (p.in_scale) v = act_fwd(p.in_act, v * p.in_scale[ci] + p.in_shift[ci]);
-    return v;
-  }
-  return p.x2[pix * p.c2 + (ci - p.c1)];
+// ---- operand fetch: raw buffer loads through wave-uniform descriptors. An out-of-range offset
+// (OOB) returns zeros, so padding taps, ragged tiles and the idle source of a concat need no
+// branch around the load: every load of a K-step issues back to back and nothing waits on it
+// until the tile is written to LDS after the MFMAs (the input prologue is applied there too).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned OOB = 0x80000000u;
+constexpr long MAX_RECORDS = 0x7FFFFFF0L;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, long bytes) {
+  const int n = (int)(bytes < MAX_RECORDS ? (bytes > 0 ? bytes : 0) : MAX_RECORDS);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
 }
 
-__device__ __forceinline__ float4 load_x4(const GemmConvParams& p, int img, int iy, int ix,
-                                          int ci) {
-  if (iy < 0 || iy >= p.h || ix < 0 || ix >= p.w) return make_float4(0.f, 0.f, 0.f, 0.f);
-  const long pix = ((long)img * p.h + iy) * p.w + ix;
-  if (ci < p.c1) {
-    float4 v = *reinterpret_cast<const float4*>(p.x1 + pix * p.c1 + ci);
-    if (p.in_scale) {
-      const float4 s = *reinterpret_cast<const float4*>(p.in_scale + ci);
-      const float4 t = *reinterpret_cast<const float4*>(p.in_shift + ci);
-      v.x = act_fwd(p.in_act, v.x * s.x + t.x);
-      v.y = act_fwd(p.in_act, v.y * s.y + t.y);
-      v.z = act_fwd(p.in_act, v.z * s.z + t.z);
-      v.w = act_fwd(p.in_act, v.w * s.w + t.w);
-    }
-    return v;
-  }
-  return *reinterpret_cast<const float4*>(p.x2 + pix * p.c2 + (ci - p.c1));
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__device__ __forceinline__ float4 prologue4(int act, float4 v, float4 s, float4 t) {
+  return make_float4(act_fwd(act, v.x * s.x + t.x), act_fwd(act, v.y * s.y + t.y),
+                     act_fwd(act, v.z * s.z + t.z), act_fwd(act, v.w * s.w + t.w));
 }
 
 template <int BM, int BN, int WM, int WN, int MODE, bool VEC, bool VEC16>
@@ -112,6 +111,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
     kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
   }
 
+  // ------------------------------------------------------------------ descriptors
+  // x1/x2 are addressed relative to the first image this workgroup touches, so offsets stay
+  // 32-bit for any batch (the host bounds the span one workgroup can reach).
+  int img_base, pix_base = 0;
+  if (MODE == MODE_FWD) {
+    img_base = (int)p.dOH.div(p.dOW.div((uint32_t)m0));
+  } else {
+    pix_base = kt_begin * BK;
+    img_base = (int)p.dOH.div(p.dOW.div((uint32_t)min(pix_base, p.K - 1)));
+  }
+  const long img_elems = (long)p.h * p.w;
+  const __amdgpu_buffer_rsrc_t rs1 =
+      make_rsrc(p.x1 + img_base * img_elems * p.c1, (p.n - img_base) * img_elems * p.c1 * 4);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      p.c2 ? make_rsrc(p.x2 + img_base * img_elems * p.c2, (p.n - img_base) * img_elems * p.c2 * 4)
+           : make_rsrc(p.x1, 0);
+  const __amdgpu_buffer_rsrc_t rsb =
+      (MODE == MODE_FWD) ? make_rsrc(p.bmat, (long)p.N * p.K * 4)
+                         : make_rsrc(p.bmat + (long)pix_base * p.N, (long)(p.K - pix_base) * p.N * 4);
+
   // ------------------------------------------------------------------ staging registers
   // FWD A: BM rows x 4 float4 ; thread -> (row = tid/4 + 64 j, kq = tid%4)
   // FWD B: BN rows x 4 float4 ; same mapping, rows < BN
@@ -119,109 +138,178 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
   // WGRAD B: 16 k-rows x BN/4 float4
   constexpr int A_V4 = BM * BK / 4, B_V4 = BN * BK / 4;
   constexpr int A_PER = (A_V4 + 255) / 256, B_PER = (B_V4 + 255) / 256;
+  constexpr bool DUAL = !VEC16;  // separate source-2 staging (concat whose K-steps mix sources)
   float4 ra[A_PER], rb[B_PER];
+  float4 ra2[DUAL ? A_PER : 1];
+  unsigned vmask = 0;  // valid (in-image) elements of the staged A tile: prologue targets
+  unsigned pmask = 0;  // elements from source 1 (prologue applies) — scalar paths
+  float4 psc = make_float4(0.f, 0.f, 0.f, 0.f), psh = psc;  // prologue scale/shift (VEC paths)
+  float esc[4] = {0.f, 0.f, 0.f, 0.f}, esh[4] = {0.f, 0.f, 0.f, 0.f};  // (scalar paths)
+  bool pro = false;
+  const int kq = tid & 3;
 
-  // per-thread constants
-  // FWD: pixel decomposition of this thread's A rows
-  int a_img[A_PER], a_iy0[A_PER], a_ix0[A_PER];
+  // per-thread constants. FWD: pixel decomposition of this thread's A rows
+  int a_ir[A_PER], a_iy0[A_PER], a_ix0[A_PER];
   bool a_ok[A_PER];
-  // WGRAD: tap/channel decomposition of this thread's A column group
-  int w_ty = 0, w_tx = 0, w_ci = 0;
-  bool w_iok = false;
+  // WGRAD: tap/channel decomposition of this thread's A column group (per element when !VEC)
+  int w_ty[4], w_tx[4], w_ci[4];
+  bool w_ok[4];
   if (MODE == MODE_FWD) {
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
       const int v = tid + 256 * j;
       const int m = m0 + v / 4;
       a_ok[j] = (v < A_V4) && (m < p.M);
-      const int mm = a_ok[j] ? m : 0;
+      const int mm = a_ok[j] ? m : m0;
       const uint32_t q = p.dOW.div((uint32_t)mm);
       const int ox = mm - (int)q * p.ow;
       const uint32_t img = p.dOH.div(q);
       const int oy = (int)q - (int)img * p.oh;
-      a_img[j] = (int)img;
+      a_ir[j] = ((int)img - img_base) * p.h;
       a_iy0[j] = oy * p.sh - p.pt;
       a_ix0[j] = ox * p.sw - p.pl;
     }
   } else {
-    const int i = m0 + 4 * (tid % (BM / 4));
-    w_iok = i < p.M;
-    const int ii = w_iok ? i : 0;
-    const uint32_t tap = p.dC.div((uint32_t)ii);
-    w_ci = ii - (int)tap * p.C;
-    const uint32_t ty = p.dKW.div(tap);
-    w_ty = (int)ty;
-    w_tx = (int)tap - (int)ty * p.kw;
+    const int i0 = m0 + 4 * (tid % (BM / 4));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + (VEC ? 0 : u);
+      w_ok[u] = i < p.M;
+      const int ii = w_ok[u] ? i : 0;
+      const uint32_t tap = p.dC.div((uint32_t)ii);
+      w_ci[u] = ii - (int)tap * p.C;
+      const uint32_t ty = p.dKW.div(tap);
+      w_ty[u] = (int)ty;
+      w_tx[u] = (int)tap - (int)ty * p.kw;
+    }
+    if (p.in_scale) {  // a thread's channels are fixed in WGRAD: fetch the prologue once
+      if (VEC) {
+        pro = w_ok[0] && w_ci[0] < p.c1;
+        if (pro) {
+          psc = *reinterpret_cast<const float4*>(p.in_scale + w_ci[0]);
+          psh = *reinterpret_cast<const float4*>(p.in_shift + w_ci[0]);
+        }
+      } else {
+        pro = true;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (w_ok[u] && w_ci[u] < p.c1) {
+            esc[u] = p.in_scale[w_ci[u]];
+            esh[u] = p.in_shift[w_ci[u]];
+          }
+      }
+    }
   }
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
-    int s_ty = 0, s_tx = 0, s_ci = 0;
-    if (MODE == MODE_FWD && VEC16) {
-      const int tap = (int)p.dC.div((uint32_t)k0);
-      s_ci = k0 - tap * p.C;
-      s_ty = (int)p.dKW.div((uint32_t)tap);
-      s_tx = tap - s_ty * p.kw;
-    }
+    vmask = 0;
+    pmask = 0;
     if (MODE == MODE_FWD) {
+      if (VEC16) {
+        // C % 16 == 0 and c1 % 16 == 0: the whole 16-wide K-step sits in one tap and one source;
+        // its decomposition (and the descriptor choice) is wave-uniform
+        const int tap = (int)p.dC.div((uint32_t)k0);
+        const int ci = k0 - tap * p.C;
+        const int ty = (int)p.dKW.div((uint32_t)tap);
+        const int tx = tap - ty * p.kw;
+        const bool src2 = ci >= p.c1;
+        const int cs = src2 ? p.c2 : p.c1;
+        const int cb = (src2 ? ci - p.c1 : ci) + 4 * kq;
+        const __amdgpu_buffer_rsrc_t rs = src2 ? rs2 : rs1;
 #pragma unroll
-      for (int j = 0; j < A_PER; ++j) {
-        const int v = tid + 256 * j;
-        const int kq = v & 3;
+        for (int j = 0; j < A_PER; ++j) {
+          const int iy = a_iy0[j] + ty, ix = a_ix0[j] + tx;
+          const bool ok = a_ok[j] && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+          const unsigned off = ok ? (unsigned)((((a_ir[j] + iy) * p.w + ix) * cs + cb) * 4) : OOB;
+          ra[j] = bload4(rs, off);
+          vmask |= (unsigned)ok << j;
+        }
+        pro = p.in_scale && !src2;
+        if (pro) {
+          psc = *reinterpret_cast<const float4*>(p.in_scale + cb);
+          psh = *reinterpret_cast<const float4*>(p.in_shift + cb);
+        }
+      } else if (VEC) {
         const int k = k0 + 4 * kq;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a_ok[j]) {
-          if (VEC16) {
-            // C % 16 == 0 and c1 % 16 == 0: the whole 16-wide K-step sits in one tap and one
-            // source; its decomposition is wave-uniform (computed once above)
-            if (k0 < p.K)
-              val = load_x4(p, a_img[j], a_iy0[j] + s_ty, a_ix0[j] + s_tx, s_ci + 4 * kq);
-          } else if (VEC) {
-            if (k < p.K) {
-              const uint32_t tap = p.dC.div((uint32_t)k);
-              const int ci = k - (int)tap * p.C;
-              const uint32_t ty = p.dKW.div(tap);
-              const int tx = (int)tap - (int)ty * p.kw;
-              val = load_x4(p, a_img[j], a_iy0[j] + (int)ty, a_ix0[j] + tx, ci);
-            }
-          } else {
-            float e[4];
+        const bool kin = k < p.K;
+        const int kk = kin ? k : 0;
+        const int tap = (int)p.dC.div((uint32_t)kk);
+        const int ci = kk - tap * p.C;
+        const int ty = (int)p.dKW.div((uint32_t)tap);
+        const int tx = tap - ty * p.kw;
+        const bool in1 = ci < p.c1;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int kk = k + u;
-              e[u] = 0.f;
-              if (kk < p.K) {
-                const uint32_t tap = p.dC.div((uint32_t)kk);
-                const int ci = kk - (int)tap * p.C;
-                const uint32_t ty = p.dKW.div(tap);
-                const int tx = (int)tap - (int)ty * p.kw;
-                e[u] = load_x(p, a_img[j], a_iy0[j] + (int)ty, a_ix0[j] + tx, ci);
-              }
-            }
-            val = make_float4(e[0], e[1], e[2], e[3]);
+        for (int j = 0; j < A_PER; ++j) {
+          const int iy = a_iy0[j] + ty, ix = a_ix0[j] + tx;
+          const bool ok = kin && a_ok[j] && (unsigned)iy < (unsigned)p.h &&
+                          (unsigned)ix < (unsigned)p.w;
+          const int pix = (a_ir[j] + iy) * p.w + ix;
+          ra[j] = bload4(rs1, (ok && in1) ? (unsigned)((pix * p.c1 + ci) * 4) : OOB);
+          if (p.c2)
+            ra2[j] = bload4(rs2, (ok && !in1) ? (unsigned)((pix * p.c2 + ci - p.c1) * 4) : OOB);
+          vmask |= (unsigned)ok << j;
+        }
+        pro = p.in_scale && kin && in1;
+        if (pro) {
+          psc = *reinterpret_cast<const float4*>(p.in_scale + ci);
+          psh = *reinterpret_cast<const float4*>(p.in_shift + ci);
+        }
+      } else {
+        int ty[4], tx[4], ci[4];
+        bool kin[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + 4 * kq + u;
+          kin[u] = k < p.K;
+          const int kk = kin[u] ? k : 0;
+          const int tap = (int)p.dC.div((uint32_t)kk);
+          ci[u] = kk - tap * p.C;
+          ty[u] = (int)p.dKW.div((uint32_t)tap);
+          tx[u] = tap - ty[u] * p.kw;
+          pmask |= (unsigned)(kin[u] && ci[u] < p.c1) << u;
+          if (p.in_scale && kin[u] && ci[u] < p.c1) {
+            esc[u] = p.in_scale[ci[u]];
+            esh[u] = p.in_shift[ci[u]];
           }
         }
-        ra[j] = val;
+#pragma unroll
+        for (int j = 0; j < A_PER; ++j) {
+          float e1[4], e2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int iy = a_iy0[j] + ty[u], ix = a_ix0[j] + tx[u];
+            const bool ok = kin[u] && a_ok[j] && (unsigned)iy < (unsigned)p.h &&
+                            (unsigned)ix < (unsigned)p.w;
+            const int pix = (a_ir[j] + iy) * p.w + ix;
+            const bool in1 = ci[u] < p.c1;
+            e1[u] = bload1(rs1, (ok && in1) ? (unsigned)((pix * p.c1 + ci[u]) * 4) : OOB);
+            e2[u] = p.c2 ? bload1(rs2, (ok && !in1) ? (unsigned)((pix * p.c2 + ci[u] - p.c1) * 4)
+                                                    : OOB)
+                         : 0.f;
+            vmask |= (unsigned)ok << (4 * j + u);
+          }
+          ra[j] = make_float4(e1[0], e1[1], e1[2], e1[3]);
+          ra2[j] = make_float4(e2[0], e2[1], e2[2], e2[3]);
+        }
+        pro = p.in_scale != nullptr;
       }
 #pragma unroll
       for (int j = 0; j < B_PER; ++j) {
         const int v = tid + 256 * j;
-        const int row = v >> 2, kq = v & 3;
+        const int row = v >> 2;
         const int n = n0 + row;
         const int k = k0 + 4 * kq;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (v < B_V4 && n < p.N) {
-          const float* src = p.bmat + (long)n * p.K;
-          if (VEC) {
-            if (k < p.K) val = *reinterpret_cast<const float4*>(src + k);
-          } else {
-            val.x = (k + 0 < p.K) ? src[k + 0] : 0.f;
-            val.y = (k + 1 < p.K) ? src[k + 1] : 0.f;
-            val.z = (k + 2 < p.K) ? src[k + 2] : 0.f;
-            val.w = (k + 3 < p.K) ? src[k + 3] : 0.f;
-          }
+        const bool nok = v < B_V4 && n < p.N;
+        if (VEC) {
+          rb[j] = bload4(rsb, (nok && k < p.K) ? (unsigned)((n * p.K + k) * 4) : OOB);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            e[u] = bload1(rsb, (nok && k + u < p.K) ? (unsigned)((n * p.K + k + u) * 4) : OOB);
+          rb[j] = make_float4(e[0], e[1], e[2], e[3]);
         }
-        rb[j] = val;
       }
     } else {  // WGRAD
       constexpr int AQ = BM / 4;  // float4 per k-row
@@ -230,36 +318,42 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
       for (int j = 0; j < A_PER; ++j) {
         const int krow = tid / AQ + AROWS * j;
         const int pix = k0 + krow;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (krow < BK && pix < p.K && w_iok) {
-          const uint32_t q = p.dOW.div((uint32_t)pix);
-          const int ox = pix - (int)q * p.ow;
-          const uint32_t img = p.dOH.div(q);
-          const int oy = (int)q - (int)img * p.oh;
-          const int iy = oy * p.sh - p.pt + w_ty, ix = ox * p.sw - p.pl + w_tx;
-          if (VEC) {
-            val = load_x4(p, (int)img, iy, ix, w_ci);
-          } else {
-            // scalar path: 4 consecutive i may cross taps/sources
-            const int i0 = m0 + 4 * (tid % AQ);
-            float e[4];
+        const bool rok = krow < BK && pix < p.K;
+        const int pp = rok ? pix : pix_base;
+        const uint32_t q = p.dOW.div((uint32_t)pp);
+        const int ox = pp - (int)q * p.ow;
+        const uint32_t img = p.dOH.div(q);
+        const int oy = (int)q - (int)img * p.oh;
+        const int ir = ((int)img - img_base) * p.h;
+        if (VEC) {
+          const int iy = oy * p.sh - p.pt + w_ty[0], ix = ox * p.sw - p.pl + w_tx[0];
+          const bool ok = rok && w_ok[0] && (unsigned)iy < (unsigned)p.h &&
+                          (unsigned)ix < (unsigned)p.w;
+          const int px = (ir + iy) * p.w + ix;
+          const bool in1 = w_ci[0] < p.c1;
+          ra[j] = bload4(rs1, (ok && in1) ? (unsigned)((px * p.c1 + w_ci[0]) * 4) : OOB);
+          if (p.c2)
+            ra2[j] = bload4(rs2, (ok && !in1) ? (unsigned)((px * p.c2 + w_ci[0] - p.c1) * 4)
+                                              : OOB);
+          vmask |= (unsigned)ok << j;
+        } else {
+          float e1[4], e2[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int i = i0 + u;
-              e[u] = 0.f;
-              if (i < p.M) {
-                const uint32_t tap = p.dC.div((uint32_t)i);
-                const int ci = i - (int)tap * p.C;
-                const uint32_t ty = p.dKW.div(tap);
-                const int tx = (int)tap - (int)ty * p.kw;
-                e[u] = load_x(p, (int)img, oy * p.sh - p.pt + (int)ty, ox * p.sw - p.pl + tx,
-                              ci);
-              }
-            }
-            val = make_float4(e[0], e[1], e[2], e[3]);
+          for (int u = 0; u < 4; ++u) {
+            const int iy = oy * p.sh - p.pt + w_ty[u], ix = ox * p.sw - p.pl + w_tx[u];
+            const bool ok = rok && w_ok[u] && (unsigned)iy < (unsigned)p.h &&
+                            (unsigned)ix < (unsigned)p.w;
+            const int px = (ir + iy) * p.w + ix;
+            const bool in1 = w_ci[u] < p.c1;
+            e1[u] = bload1(rs1, (ok && in1) ? (unsigned)((px * p.c1 + w_ci[u]) * 4) : OOB);
+            e2[u] = p.c2 ? bload1(rs2, (ok && !in1) ? (unsigned)((px * p.c2 + w_ci[u] - p.c1) * 4)
+                                                    : OOB)
+                         : 0.f;
+            vmask |= (unsigned)ok << (4 * j + u);
           }
+          ra[j] = make_float4(e1[0], e1[1], e1[2], e1[3]);
+          ra2[j] = make_float4(e2[0], e2[1], e2[2], e2[3]);
         }
-        ra[j] = val;
       }
       constexpr int BQ = BN / 4;
       constexpr int BROWS = 256 / BQ;
@@ -268,21 +362,44 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
         const int krow = tid / BQ + BROWS * j;
         const int pix = k0 + krow;
         const int n = n0 + 4 * (tid % BQ);
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (krow < BK && pix < p.K) {
-          const float* src = p.bmat + (long)pix * p.N;
-          if ((p.N & 3) == 0) {
-            if (n < p.N) val = *reinterpret_cast<const float4*>(src + n);
-          } else {
-            val.x = (n + 0 < p.N) ? src[n + 0] : 0.f;
-            val.y = (n + 1 < p.N) ? src[n + 1] : 0.f;
-            val.z = (n + 2 < p.N) ? src[n + 2] : 0.f;
-            val.w = (n + 3 < p.N) ? src[n + 3] : 0.f;
-          }
+        const bool rok = krow < BK && pix < p.K;
+        const int rel = (pix - pix_base) * p.N + n;
+        if ((p.N & 3) == 0) {
+          rb[j] = bload4(rsb, (rok && n < p.N) ? (unsigned)(rel * 4) : OOB);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            e[u] = bload1(rsb, (rok && n + u < p.N) ? (unsigned)((rel + u) * 4) : OOB);
+          rb[j] = make_float4(e[0], e[1], e[2], e[3]);
         }
-        rb[j] = val;
       }
     }
+  };
+
+  // staged A value for LDS: the prologue act(x*scale+shift) on in-image source-1 elements
+  // (padding taps stay 0: TF pads the activated tensor), plus the source-2 part
+  auto finish_a = [&](int j) -> float4 {
+    float4 v = ra[j];
+    if (VEC) {
+      if (pro && ((vmask >> j) & 1u)) v = prologue4(p.in_act, v, psc, psh);
+    } else {
+      if (pro) {
+        float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned bit = (MODE == MODE_FWD) ? ((pmask >> u) & 1u)
+                                                  : (unsigned)(w_ok[u] && w_ci[u] < p.c1);
+          if (bit && ((vmask >> (4 * j + u)) & 1u))
+            e[u] = act_fwd(p.in_act, e[u] * esc[u] + esh[u]);
+        }
+        v = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    if constexpr (DUAL) {
+      if (p.c2) v = add4(v, ra2[j]);
+    }
+    return v;
   };
 
   auto store_tile = [&](int buf) {
@@ -291,7 +408,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
       for (int j = 0; j < A_PER; ++j) {
         const int v = tid + 256 * j;
         if (v < A_V4)
-          *reinterpret_cast<float4*>(As(buf) + (v >> 2) * (BK + PADK) + 4 * (v & 3)) = ra[j];
+          *reinterpret_cast<float4*>(As(buf) + (v >> 2) * (BK + PADK) + 4 * (v & 3)) =
+              finish_a(j);
       }
 #pragma unroll
       for (int j = 0; j < B_PER; ++j) {
@@ -305,7 +423,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
       for (int j = 0; j < A_PER; ++j) {
         const int krow = tid / AQ + AROWS * j;
         if (krow < BK)
-          *reinterpret_cast<float4*>(As(buf) + krow * (BM + PADK) + 4 * (tid % AQ)) = ra[j];
+          *reinterpret_cast<float4*>(As(buf) + krow * (BM + PADK) + 4 * (tid % AQ)) = finish_a(j);
       }
       constexpr int BQ = BN / 4, BROWS = 256 / BQ;
 #pragma unroll
@@ -335,8 +453,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
   __syncthreads();
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = (kt - kt_begin) & 1;
-    const bool more = kt + 1 < kt_end;
-    if (more) load_tile(kt + 1);
+    // the next tile's loads issue unconditionally (the last step re-fetches its own tile into
+    // the idle buffer): no loop-carried select on the staging registers, so nothing waits on
+    // the loads until store_tile after the MFMAs
+    load_tile(kt + 1 < kt_end ? kt + 1 : kt);
     const float* A = As(buf);
     const float* Bm = Bs(buf);
     float af[TM][8], bf[TN][8];
@@ -375,7 +495,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bf[b][kk], acc[a][b], 0, 0, 0);
-    if (more) store_tile(buf ^ 1);
+    store_tile(buf ^ 1);
     __syncthreads();
   }
 
@@ -640,10 +760,19 @@ static void fwd_split_plan(long M, long N, long K, int tile, int& cfg, int& spli
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
 
+// bytes one workgroup's A operand can span from its base image (buffer offsets are 32-bit)
+static long fwd_span_bytes(const GemmConvParams& p, int bm) {
+  const long imgs = bm / ((long)p.oh * p.ow) + 2;
+  return imgs * p.h * p.w * (long)std::max(p.c1, p.c2) * 4;
+}
+
 static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void* ws,
                         size_t ws_bytes, hipStream_t st, const char* who) {
   int cfg, splits, kt_per;
   fwd_split_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+  PLD_CHECK_ARG(fwd_span_bytes(p, kTiles[cfg].bm) < MAX_RECORDS &&
+                    (long)p.N * p.K * 4 < MAX_RECORDS,
+                "%s: image or filter too large for 32-bit buffer offsets", who);
   if (splits == 1) {
     p.ktiles_per_split = 0;
     p.zstride = 0;
@@ -846,6 +975,16 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
   const long tiles = (long)cdiv(M, kTiles[cfg].bm) * cdiv(N, kTiles[cfg].bn);
   long s = std::max<long>(1, (768 + tiles - 1) / tiles);
   s = std::min<long>(s, std::max<long>(1, ktiles / 8));  // >= 8 k-steps per block
+  // a workgroup's pixel range must stay within 32-bit buffer offsets of its base image
+  const long img_in = (long)a->h * a->w * std::max(a->c1, a->c2) * 4;
+  const long img_out = (long)a->oh * a->ow;
+  for (;;) {
+    const long kp = (ktiles + s - 1) / s;
+    const long span_a = (kp * BK / img_out + 2) * img_in;
+    const long span_b = kp * BK * (long)N * 4;
+    if ((span_a < MAX_RECORDS && span_b < MAX_RECORDS) || kp <= 1) break;
+    ++s;
+  }
   kt_per = (int)((ktiles + s - 1) / s);
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
