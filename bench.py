@@ -51,10 +51,8 @@ def profile_conv(trainer, lr):
     orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad")}
 
     def flops_of(name, a):
-        C = a.c1 + a.c2
-        if name == "conv2d_dgrad":
-            return 2.0 * a.n * a.h * a.w * C * a.kh * a.kw * a.cout
-        return 2.0 * a.n * a.oh * a.ow * a.cout * a.kh * a.kw * C
+        # fwd, dX and dW of one conv are the same contraction: 2 * outputs * taps * Cin * Cout
+        return 2.0 * a.n * a.oh * a.ow * a.cout * a.kh * a.kw * (a.c1 + a.c2)
 
     def wrap(name):
         fn = orig[name]
