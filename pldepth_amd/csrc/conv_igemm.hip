@@ -554,6 +554,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// first level of a two-level ordered reduction for many split-K slabs: group g sums slabs
+// [g*per, (g+1)*per) in order into part[g][i] (enough threads when M*N is small and splits many)
+constexpr int SPLIT_GROUP = 16;
+
+__global__ __launch_bounds__(256) void splitk_group_kernel(const float* __restrict__ ws,
+                                                           int splits, long n,
+                                                           float* __restrict__ part) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int z0 = blockIdx.y * SPLIT_GROUP, z1 = min(splits, z0 + SPLIT_GROUP);
+  float s = 0.f;
+  for (int z = z0; z < z1; ++z) s += ws[(long)z * n + i];
+  part[(long)blockIdx.y * n + i] = s;
+}
+
 // ordered split-K reduction of forward / dgrad slabs with bias and two-destination routing
 __global__ __launch_bounds__(256) void splitk_out_kernel(const float* __restrict__ ws, int splits,
                                                          long M, int N, const float* bias,
@@ -641,10 +656,12 @@ __global__ void filter_dgrad_kernel(const float* __restrict__ w, int kh, int kw,
 // ------------------------------------------------------------------------ dispatch
 // ---- tile configurations and a small cost model ----
 // (BM, BN, WM, WN): 4 waves; each wave computes (BM/WM) x (BN/WN) as 32x32 MFMA tiles.
-struct TileCfg { int bm, bn, tm, tn; };
+// occ: resident blocks per CU (VGPR/AGPR bound, from the compiler's resource report)
+struct TileCfg { int bm, bn, tm, tn, occ; };
 static const TileCfg kTiles[] = {
-    {256, 32, 2, 1},  {128, 64, 1, 1},  {128, 96, 1, 3},  {128, 128, 2, 2},
-    {128, 160, 1, 5}, {128, 192, 1, 6}, {128, 224, 1, 7},
+    {256, 32, 2, 1, 3},  {128, 64, 1, 1, 4},  {128, 96, 1, 3, 4},  {128, 128, 2, 2, 3},
+    {128, 160, 1, 5, 2}, {128, 192, 1, 6, 2}, {128, 224, 1, 7, 2}, {256, 64, 2, 2, 3},
+    {256, 128, 4, 2, 1},
 };
 
 // estimated relative time: padded MFMA work per block x waves of blocks over 256 CUs,
@@ -664,7 +681,7 @@ static int choose_tile(long M, long N, long K, int splits, int requested = -1) {
     const long blocks = (long)cdiv(M, t.bm) * cdiv(N, t.bn) * splits;
     const int per_wave = t.tm * t.tn;
     const double eff = per_wave >= 4 ? 1.0 : (per_wave == 3 ? 0.9 : (per_wave == 2 ? 0.8 : 0.55));
-    const int occ = (t.bn >= 160) ? 2 : 3;  // resident blocks per CU (VGPR bound)
+    const int occ = t.occ;
     const double rounds = std::ceil((double)blocks / (256.0 * occ));
     const double t_est = rounds * occ * (double)t.bm * t.bn * ((double)K / splits) / eff;
     if (t_est < best_t * 0.97) {
@@ -694,7 +711,9 @@ static int launch_igemm(GemmConvParams& p, bool vec, bool vec16, int splits, int
     case 3: launch_cfg<MODE, 128, 128, 2, 2>(p, vec, vec16, splits, st); break;
     case 4: launch_cfg<MODE, 128, 160, 4, 1>(p, vec, vec16, splits, st); break;
     case 5: launch_cfg<MODE, 128, 192, 4, 1>(p, vec, vec16, splits, st); break;
-    default: launch_cfg<MODE, 128, 224, 4, 1>(p, vec, vec16, splits, st); break;
+    case 6: launch_cfg<MODE, 128, 224, 4, 1>(p, vec, vec16, splits, st); break;
+    case 7: launch_cfg<MODE, 256, 64, 4, 1>(p, vec, vec16, splits, st); break;
+    default: launch_cfg<MODE, 256, 128, 2, 2>(p, vec, vec16, splits, st); break;
   }
   return check_launch("conv_igemm_kernel");
 }
@@ -989,6 +1008,13 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
 
+// split-K slabs + the first-level group partials of the two-level reduction
+static size_t wgrad_ws_bytes(int splits, int M, int N) {
+  if (splits <= 1) return 0;
+  const int groups = splits > 2 * SPLIT_GROUP ? (splits + SPLIT_GROUP - 1) / SPLIT_GROUP : 0;
+  return sizeof(float) * (size_t)(splits + groups) * M * N;
+}
+
 extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->kh <= 0 || a->kw <= 0 || a->c1 <= 0 || a->c2 < 0 || a->cout <= 0 ||
       a->oh <= 0 || a->ow <= 0)
@@ -997,7 +1023,7 @@ extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
   int M, N, splits, kt, cfg;
   long K;
   wgrad_plan(a, M, N, K, splits, kt, cfg);
-  return splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  return wgrad_ws_bytes(splits, M, N);
 }
 
 extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* dw,
@@ -1016,7 +1042,7 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   long K;
   wgrad_plan(a, M, N, K, splits, kt_per, cfg);
   PLD_CHECK_ARG(K < (1L << 31), "pld_conv2d_wgrad: too many pixels");
-  const size_t need = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  const size_t need = wgrad_ws_bytes(splits, M, N);
   PLD_CHECK_ARG(ws_bytes >= need && (need == 0 || ws),
                 "pld_conv2d_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
   p.bmat = dy;
@@ -1044,7 +1070,18 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   rc = launch_igemm<MODE_WGRAD>(p, vec, false, splits, cfg, st);
   if (rc || splits == 1) return rc;
   const long n = (long)M * N;
+  const float* src = (const float*)ws;
+  int terms = splits;
+  if (splits > 2 * SPLIT_GROUP) {
+    const int groups = (splits + SPLIT_GROUP - 1) / SPLIT_GROUP;
+    float* part = (float*)ws + (long)splits * n;
+    splitk_group_kernel<<<dim3(cdiv(n, 256), groups), 256, 0, st>>>(src, splits, n, part);
+    rc = check_launch("splitk_group_kernel");
+    if (rc) return rc;
+    src = part;
+    terms = groups;
+  }
   splitk_reduce_kernel<<<std::min<unsigned>(cdiv(n, 256), 4096), 256, 0, st>>>(
-      (const float*)ws, splits, n, dw, accumulate);
+      src, terms, n, dw, accumulate);
   return check_launch("splitk_reduce_kernel");
 }
