@@ -177,6 +177,9 @@ def main():
                     help="ff_redweb = the ResNet-50 backbone (BASELINE cfg3 'ff_resnet')")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--conv-math", default="mixed", choices=["mixed", "bf16x3", "fp32"],
+                    help="conv arithmetic policy (kernels.conv_policy): mixed = encoder fp32, "
+                         "decoder bf16x3")
     ap.add_argument("--tile-cache", default="",
                     help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
@@ -194,6 +197,8 @@ def main():
         pg = dist.group.WORLD
 
     from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
+    from pldepth_amd import kernels as K
+    K.set_conv_math(a.conv_math)
     from pldepth_amd.trainer import ReplicaTrainer
 
     H = W = a.size

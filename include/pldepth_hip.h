@@ -77,7 +77,7 @@ int pld_step_increment(int64_t* step_dev, void* stream);
 int pld_set_scalar_f32(float* dev, float value, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * Convolution (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32): replaces Keras Conv2D /
+ * Convolution (implicit GEMM on MFMA, fp32 in/out; see pld_conv_args.math): replaces Keras Conv2D /
  * TF Conv2D + Conv2DBackpropInput + Conv2DBackpropFilter (pl_hourglass.py:59-96 decoder, the
  * EfficientNetB0 1x1/3x3 convs, redweb.py convs). The input may be the channel concatenation of
  * two NHWC tensors (layers.Concatenate, pl_hourglass.py:66,75,84) — no concat is materialised.
@@ -106,10 +106,24 @@ typedef struct pld_conv_args {
    * pld_conv2d_{fwd,dgrad}_workspace_size; may be NULL when that size is 0) */
   void* ws;
   size_t ws_bytes;
+  /* product arithmetic (PLD_MATH_*): FP32 = v_mfma_f32_32x32x2_f32, exact fp32 fmaf chains;
+   * BF16X3 = each fp32 operand split into bf16 hi + lo and a.b = a_hi.b_hi + a_hi.b_lo +
+   * a_lo.b_hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (|error| <= ~2^-16 |a.b| per
+   * product; 5.3x the fp32 MFMA rate). Shapes the BF16X3 kernel does not take (channel counts
+   * not a multiple of 8 for fwd/dgrad, of 4 for wgrad) run on the FP32 path. */
+  int math;
+  /* optional, BF16X3 fwd/dgrad only: the filter operand (w_ohwi for fwd, w_dgrad for dgrad)
+   * already split by pld_filter_split, so the kernel stages it without converting; NULL = the
+   * kernel splits the fp32 filter itself. Ignored on the FP32 path. */
+  const void* w_split;
 } pld_conv_args;
 
-/* number of implicit-GEMM schedules selectable through pld_conv_args.tile */
+enum { PLD_MATH_FP32 = 0, PLD_MATH_BF16X3 = 1 };
+
+/* number of implicit-GEMM schedules selectable through pld_conv_args.tile (FP32 math) */
 int pld_conv_num_tiles(void);
+/* the same for a given PLD_MATH_* */
+int pld_conv_num_schedules(int math);
 size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a);
 size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a);
 
@@ -131,6 +145,12 @@ int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgr
 size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a);
 int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* dw, int accumulate, void* ws,
                      size_t ws_bytes, void* stream);
+
+/* bf16x3 operand split of a row-major [rows][K] fp32 matrix (K % 8 == 0), e.g. a native or
+ * dgrad filter: every 8 consecutive values v become 8 bf16 hi = rne(v) then 8 bf16 lo =
+ * rne(v - hi) — 32 bytes, the size and offset of the 8 fp32 values they replace (pld_conv_args
+ * .w_split). */
+int pld_filter_split(const float* w, int64_t rows, int K, void* out, void* stream);
 
 /* HWIO [kh][kw][cin][cout] -> forward native [cout][kh][kw][cin] */
 int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_ohwi,

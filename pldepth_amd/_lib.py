@@ -31,7 +31,7 @@ class ConvArgs(C.Structure):
         ("kh", I32), ("kw", I32), ("sh", I32), ("sw", I32), ("pad_t", I32), ("pad_l", I32),
         ("oh", I32), ("ow", I32), ("cout", I32),
         ("in_scale", P), ("in_shift", P), ("in_act", I32), ("tile", I32),
-        ("ws", P), ("ws_bytes", SZ),
+        ("ws", P), ("ws_bytes", SZ), ("math", I32), ("w_split", P),
     ]
 
 
@@ -50,9 +50,11 @@ _SIGS = {
     "pld_conv2d_wgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_wgrad": (I32, [C.POINTER(ConvArgs), P, P, I32, P, SZ, P]),
     "pld_conv_num_tiles": (I32, []),
+    "pld_conv_num_schedules": (I32, [I32]),
     "pld_conv2d_fwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_dgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_filter_to_native": (I32, [P, I32, I32, I32, I32, P, P]),
+    "pld_filter_split": (I32, [P, I64, I32, P, P]),
     "pld_filter_to_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_channel_reduce_workspace_size": (SZ, [I64, I32]),
     "pld_channel_sum": (I32, [P, I64, I32, P, I32, P, P]),
@@ -89,7 +91,7 @@ _SIGS = {
 }
 
 # functions returning a value rather than a status
-_NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles",
+_NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_num_schedules",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates"}

@@ -1,0 +1,113 @@
+// Shared pieces of the implicit-GEMM convolution kernels (conv_igemm.hip: exact fp32 MFMA;
+// conv_x3.hip: fp32 through three bf16 MFMA products): the GEMM view of one NHWC convolution,
+// buffer-descriptor operand fetch, the fused input prologue and the accumulator epilogue.
+#pragma once
+#include "common.h"
+
+namespace pld {
+
+enum ConvMode { MODE_FWD = 0, MODE_WGRAD = 1 };
+
+// One NHWC convolution seen as C[M][N] = A[M][K] . B[K][N]:
+//   FWD   : m = (img,oy,ox), n = co, k = (ty,tx,ci); A = im2col(x1 ++ x2), B = Wn^T ([N][K])
+//   DGRAD : FWD on (dY, flipped filter), output columns routed to dx1 / dx2 at `split`
+//   WGRAD : m = (ty,tx,ci), n = co, k = (img,oy,ox) pixels; A = im2col^T, B = dY ([K][N])
+struct GemmConvParams {
+  const float* x1;
+  const float* x2;
+  int c1, c2, C;
+  int n, h, w, kh, kw, sh, sw, pt, pl, oh, ow;
+  const float* in_scale;
+  const float* in_shift;
+  int in_act;
+  const float* bmat;    // FWD: Wn [N][K]; WGRAD: dY [K][N]
+  const float* bsplit;  // FWD, bf16x3 kernel only: Wn pre-split (pld_filter_split) or NULL
+  int M, N, K;
+  const float* bias;
+  float* out1;
+  int ld1, acc1;
+  float* out2;
+  int ld2, acc2, split;
+  long zstride;
+  int ktiles_per_split;
+  FastDiv dC, dKW, dOW, dOH;
+};
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---- operand fetch: raw buffer loads through wave-uniform descriptors. An out-of-range offset
+// (OOB) returns zeros, so padding taps, ragged tiles and the idle source of a concat need no
+// branch around the load.
+constexpr unsigned OOB = 0x80000000u;
+constexpr long MAX_RECORDS = 0x7FFFFFF0L;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, long bytes) {
+  const int n = (int)(bytes < MAX_RECORDS ? (bytes > 0 ? bytes : 0) : MAX_RECORDS);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
+}
+
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__device__ __forceinline__ float4 prologue4(int act, float4 v, float4 s, float4 t) {
+  return make_float4(act_fwd(act, v.x * s.x + t.x), act_fwd(act, v.y * s.y + t.y),
+                     act_fwd(act, v.z * s.z + t.z), act_fwd(act, v.w * s.w + t.w));
+}
+
+// ---- epilogue of a wave's TM x TN grid of 32x32 accumulators (C/D map of the 32x32 MFMA
+// forms: column = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)). m_w/n_w: the wave's first
+// output row/column. Split-K slabs (zstride > 0) get the raw sums; otherwise bias, two-way
+// column routing (dgrad of a concat) and accumulate-or-overwrite are applied.
+template <int TM, int TN>
+__device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx16 (&acc)[TM][TN],
+                                          int m_w, int n_w, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+  if (p.zstride > 0) {
+    float* out1 = p.out1 + (long)blockIdx.z * p.zstride;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n_w + b * 32 + l32;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < p.M) out1[(long)row * p.N + col] = acc[a][b][r];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n_w + b * 32 + l32;
+      if (col >= p.N) continue;
+      const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        const float v = acc[a][b][r] + bias;
+        if (col < p.split) {
+          float* dst = p.out1 + (long)row * p.ld1 + col;
+          *dst = p.acc1 ? *dst + v : v;
+        } else {
+          float* dst = p.out2 + (long)row * p.ld2 + (col - p.split);
+          *dst = p.acc2 ? *dst + v : v;
+        }
+      }
+    }
+}
+
+}  // namespace pld

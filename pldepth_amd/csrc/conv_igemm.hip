@@ -24,66 +24,12 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "common.h"
+#include "conv_common.h"
 
 namespace pld {
 
-enum ConvMode { MODE_FWD = 0, MODE_WGRAD = 1 };
-
-struct GemmConvParams {
-  const float* x1;
-  const float* x2;
-  int c1, c2, C;
-  int n, h, w, kh, kw, sh, sw, pt, pl, oh, ow;
-  const float* in_scale;
-  const float* in_shift;
-  int in_act;
-  const float* bmat;  // FWD: Wn [N][K]; WGRAD: dY [K][N]
-  int M, N, K;
-  const float* bias;
-  float* out1;
-  int ld1, acc1;
-  float* out2;
-  int ld2, acc2, split;
-  long zstride;
-  int ktiles_per_split;
-  FastDiv dC, dKW, dOW, dOH;
-};
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
 constexpr int BK = 16;
 constexpr int PADK = 4;  // [row][BK+PADK]: 80-byte rows -> conflict-free b128 fragment reads
-
-// ---- operand fetch: raw buffer loads through wave-uniform descriptors. An out-of-range offset
-// (OOB) returns zeros, so padding taps, ragged tiles and the idle source of a concat need no
-// branch around the load: every load of a K-step issues back to back and nothing waits on it
-// until the tile is written to LDS after the MFMAs (the input prologue is applied there too).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr unsigned OOB = 0x80000000u;
-constexpr long MAX_RECORDS = 0x7FFFFFF0L;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, long bytes) {
-  const int n = (int)(bytes < MAX_RECORDS ? (bytes > 0 ? bytes : 0) : MAX_RECORDS);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, n, 0x00020000);
-}
-
-__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-
-__device__ __forceinline__ float4 add4(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-
-__device__ __forceinline__ float4 prologue4(int act, float4 v, float4 s, float4 t) {
-  return make_float4(act_fwd(act, v.x * s.x + t.x), act_fwd(act, v.y * s.y + t.y),
-                     act_fwd(act, v.z * s.z + t.z), act_fwd(act, v.w * s.w + t.w));
-}
 
 template <int BM, int BN, int WM, int WN, int MODE, bool VEC, bool VEC16>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
@@ -313,10 +259,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
       }
     } else {  // WGRAD
       constexpr int AQ = BM / 4;  // float4 per k-row
-      constexpr int AROWS = 256 / AQ;
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
-        const int krow = tid / AQ + AROWS * j;
+        const int krow = (tid + 256 * j) / AQ;
         const int pix = k0 + krow;
         const bool rok = krow < BK && pix < p.K;
         const int pp = rok ? pix : pix_base;
@@ -356,12 +301,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
         }
       }
       constexpr int BQ = BN / 4;
-      constexpr int BROWS = 256 / BQ;
 #pragma unroll
       for (int j = 0; j < B_PER; ++j) {
-        const int krow = tid / BQ + BROWS * j;
+        // linear float4 slot v -> (k-row, column quad): covers all BK x BQ slots for any BN
+        const int krow = (tid + 256 * j) / BQ;
         const int pix = k0 + krow;
-        const int n = n0 + 4 * (tid % BQ);
+        const int n = n0 + 4 * ((tid + 256 * j) % BQ);
         const bool rok = krow < BK && pix < p.K;
         const int rel = (pix - pix_base) * p.N + n;
         if ((p.N & 3) == 0) {
@@ -418,19 +363,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
           *reinterpret_cast<float4*>(Bs(buf) + (v >> 2) * (BK + PADK) + 4 * (v & 3)) = rb[j];
       }
     } else {
-      constexpr int AQ = BM / 4, AROWS = 256 / AQ;
+      constexpr int AQ = BM / 4;
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
-        const int krow = tid / AQ + AROWS * j;
-        if (krow < BK)
-          *reinterpret_cast<float4*>(As(buf) + krow * (BM + PADK) + 4 * (tid % AQ)) = finish_a(j);
+        const int v = tid + 256 * j;
+        if (v / AQ < BK)
+          *reinterpret_cast<float4*>(As(buf) + (v / AQ) * (BM + PADK) + 4 * (v % AQ)) = finish_a(j);
       }
-      constexpr int BQ = BN / 4, BROWS = 256 / BQ;
+      constexpr int BQ = BN / 4;
 #pragma unroll
       for (int j = 0; j < B_PER; ++j) {
-        const int krow = tid / BQ + BROWS * j;
-        if (krow < BK)
-          *reinterpret_cast<float4*>(Bs(buf) + krow * (BN + PADK) + 4 * (tid % BQ)) = rb[j];
+        const int v = tid + 256 * j;
+        if (v / BQ < BK)
+          *reinterpret_cast<float4*>(Bs(buf) + (v / BQ) * (BN + PADK) + 4 * (v % BQ)) = rb[j];
       }
     }
   };
@@ -501,45 +446,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
 
 #undef As
 #undef Bs
-  // ------------------------------------------------------------------ epilogue
-  float* out1 = p.out1;
-  if (p.zstride > 0) {  // split-K partial slab [z][M][N], reduced (+bias, routing) afterwards
-    out1 += (long)blockIdx.z * p.zstride;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = n0 + wn * WTN + b * 32 + l32;
-        if (col >= p.N) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row < p.M) out1[(long)row * p.N + col] = acc[a][b][r];
-        }
-      }
-    return;
-  }
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int col = n0 + wn * WTN + b * 32 + l32;
-      if (col >= p.N) continue;
-      const float bias = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        const float v = acc[a][b][r] + bias;
-        if (col < p.split) {
-          float* dst = out1 + (long)row * p.ld1 + col;
-          *dst = p.acc1 ? *dst + v : v;
-        } else {
-          float* dst = p.out2 + (long)row * p.ld2 + (col - p.split);
-          *dst = p.acc2 ? *dst + v : v;
-        }
-      }
-    }
+  store_acc<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
 }
 
 // ordered split-K reduction: dw[i] (+)= sum_z ws[z][i]
@@ -761,6 +668,77 @@ extern "C" size_t pld__skinny_wgrad_ws(const pld_conv_args* a);
 extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float* dw,
                                  int accumulate, void* ws, void* stream);
 
+// bf16x3 kernels (conv_x3.hip)
+extern "C" int pld__x3_num_cfg(void);
+extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int* occ);
+extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
+extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
+constexpr int X3_BK = 32;
+
+static bool x3_fwd_geom(int C, int c1) { return C % 8 == 0 && c1 % 8 == 0; }
+
+// Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), then
+// [2 n3, 2 n3 + kNumTiles) the exact-fp32 schedules — the per-shape autotuner may keep fp32
+// where it is faster (e.g. HBM-bound K <= 32 convs); it is never less accurate.
+// Resolves (math, eligible geometry, tile) to (x3 kernel?, tile in that kernel's space).
+static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t) {
+  const int nx = 2 * pld__x3_num_cfg();
+  x3 = false;
+  t = tile;
+  if (math != PLD_MATH_BF16X3) return;
+  if (tile >= nx) {
+    t = tile - nx;
+    return;
+  }
+  if (geom_ok) x3 = true;
+  else t = -1;
+}
+static bool x3_wgrad_geom(int c1, int c2, int cout) {
+  return c1 % 4 == 0 && c2 % 4 == 0 && cout % 4 == 0;
+}
+
+// the x3 analogue of choose_tile (same cost model; WGRAD takes power-of-two tiles only)
+static int x3_choose(long M, long N, long K, int requested, bool wgrad) {
+  const int n = pld__x3_num_cfg();
+  if (requested >= 0 && requested < 2 * n &&
+      (!wgrad || pld__x3_wgrad_cfg_ok(requested % n)))
+    return requested % n;
+  int best = -1;
+  double best_t = 1e300;
+  for (int i = 0; i < n; ++i) {
+    if (wgrad && !pld__x3_wgrad_cfg_ok(i)) continue;
+    int bm, bn, tm, tn, occ;
+    pld__x3_cfg_dims(i, &bm, &bn, &tm, &tn, &occ);
+    const long blocks = (long)cdiv(M, bm) * cdiv(N, bn);
+    const int per_wave = tm * tn;
+    const double eff = per_wave >= 4 ? 1.0 : (per_wave == 3 ? 0.9 : (per_wave == 2 ? 0.8 : 0.55));
+    const double rounds = std::ceil((double)blocks / (256.0 * occ));
+    const double t_est = rounds * occ * (double)bm * bn * (double)K / eff;
+    if (best < 0 || t_est < best_t * 0.97) {
+      best_t = t_est;
+      best = i;
+    }
+  }
+  return best;
+}
+
+static void x3_fwd_plan(long M, long N, long K, int tile, int& cfg, int& splits, int& kt_per) {
+  cfg = x3_choose(M, N, K, tile, false);
+  const bool allow = tile >= pld__x3_num_cfg();
+  int bm, bn, tm, tn, occ;
+  pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+  const long ktiles = (K + X3_BK - 1) / X3_BK;
+  const long blocks = (long)cdiv(M, bm) * cdiv(N, bn);
+  long s = 1;
+  if (allow) {
+    s = std::max<long>(1, (512 + blocks - 1) / blocks);
+    s = std::min<long>(s, std::max<long>(1, ktiles / 8));
+    s = std::min<long>(s, 16);
+  }
+  kt_per = (int)((ktiles + s - 1) / s);
+  splits = (int)((ktiles + kt_per - 1) / kt_per);
+}
+
 // split-K plan for a forward / dgrad GEMM under schedule `tile`: enough workgroups for ~3 per
 // CU, >= 16 K-steps each; the split-K schedules (tile >= kNumCfg) only
 static void fwd_split_plan(long M, long N, long K, int tile, int& cfg, int& splits,
@@ -786,9 +764,33 @@ static long fwd_span_bytes(const GemmConvParams& p, int bm) {
 }
 
 static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void* ws,
-                        size_t ws_bytes, hipStream_t st, const char* who) {
+                        size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
-  fwd_split_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+  bool x3;
+  resolve_sched(math, x3_fwd_geom(p.C, p.c1), tile, x3, tile);
+  if (x3) {
+    PLD_CHECK_ARG(aligned16(p.x1) && (!p.x2 || aligned16(p.x2)) && aligned16(p.bmat) &&
+                      (!p.bsplit || aligned16(p.bsplit)),
+                  "%s: bf16x3 operands must be 16-byte aligned", who);
+    x3_fwd_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+    int bm, bn, tm, tn, occ;
+    pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+    PLD_CHECK_ARG(fwd_span_bytes(p, bm) < MAX_RECORDS && (long)p.N * p.K * 4 < MAX_RECORDS,
+                  "%s: image or filter too large for 32-bit buffer offsets", who);
+  } else {
+    fwd_split_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+  }
+  auto launch = [&](GemmConvParams& q, int sp) {
+    return x3 ? pld__x3_launch(&q, MODE_FWD, sp, cfg, st)
+              : launch_igemm<MODE_FWD>(q, vec, vec16, sp, cfg, st);
+  };
+  if (x3) {
+    if (splits == 1) {
+      p.ktiles_per_split = 0;
+      p.zstride = 0;
+      return launch(p, 1);
+    }
+  } else {
   PLD_CHECK_ARG(fwd_span_bytes(p, kTiles[cfg].bm) < MAX_RECORDS &&
                     (long)p.N * p.K * 4 < MAX_RECORDS,
                 "%s: image or filter too large for 32-bit buffer offsets", who);
@@ -797,6 +799,7 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
     p.zstride = 0;
     return launch_igemm<MODE_FWD>(p, vec, vec16, 1, cfg, st);
   }
+  }
   const size_t need = sizeof(float) * (size_t)splits * p.M * p.N;
   PLD_CHECK_ARG(ws && ws_bytes >= need, "%s: split-K workspace %zu < %zu bytes", who, ws_bytes,
                 need);
@@ -804,7 +807,7 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   q.ktiles_per_split = kt_per;
   q.zstride = (long)p.M * p.N;
   q.out1 = (float*)ws;
-  int rc = launch_igemm<MODE_FWD>(q, vec, vec16, splits, cfg, st);
+  int rc = launch(q, splits);
   if (rc) return rc;
   const long n = (long)p.M * p.N;
   splitk_out_kernel<<<std::min<unsigned>(cdiv(n, 256), 8192), 256, 0, st>>>(
@@ -813,9 +816,12 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   return check_launch("splitk_out_kernel");
 }
 
-static size_t fwd_ws_bytes(long M, long N, long K, int tile) {
+static size_t fwd_ws_bytes(long M, long N, long K, int tile, int math = 0, bool geom = false) {
   int cfg, splits, kt_per;
-  fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
+  bool x3;
+  resolve_sched(math, geom, tile, x3, tile);
+  if (x3) x3_fwd_plan(M, N, K, tile, cfg, splits, kt_per);
+  else fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
   return splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
 }
 
@@ -848,6 +854,7 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   if (pld__skinny_eligible(a) && aligned16(a->x1))
     return pld__skinny_fwd(a, w_ohwi, bias, y, accumulate, stream);
   p.bmat = w_ohwi;
+  p.bsplit = (const float*)a->w_split;
   p.M = a->n * a->oh * a->ow;
   p.N = a->cout;
   p.K = a->kh * a->kw * p.C;
@@ -861,16 +868,21 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
   const bool vec16 = vec && (p.c1 % 16 == 0) && (p.c2 % 16 == 0);
   return run_fwd_gemm(p, vec, vec16, a->tile, a->ws, a->ws_bytes, as_stream(stream),
-                      "pld_conv2d_fwd");
+                      "pld_conv2d_fwd", a->math);
 }
 
 extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
+
+extern "C" int pld_conv_num_schedules(int math) {
+  return math == PLD_MATH_BF16X3 ? 2 * pld__x3_num_cfg() + kNumTiles : kNumTiles;
+}
 
 extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;
   return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
-                      (long)a->kh * a->kw * (a->c1 + a->c2), a->tile);
+                      (long)a->kh * a->kw * (a->c1 + a->c2), a->tile, a->math,
+                      x3_fwd_geom(a->c1 + a->c2, a->c1));
 }
 
 static size_t strided_tmp_bytes(const pld_conv_args* a) {
@@ -880,11 +892,12 @@ static size_t strided_tmp_bytes(const pld_conv_args* a) {
 extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->h <= 0 || a->w <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;
+  const bool geom = x3_fwd_geom(a->cout, a->cout);
   if (a->sh != 1 || a->sw != 1)  // 1x1 strided: GEMM into a compact tmp, then scatter
     return strided_tmp_bytes(a) + fwd_ws_bytes((long)a->n * a->oh * a->ow, a->c1 + a->c2,
-                                               a->cout, a->tile);
+                                               a->cout, a->tile, a->math, geom);
   return fwd_ws_bytes((long)a->n * a->h * a->w, a->c1 + a->c2, (long)a->kh * a->kw * a->cout,
-                      a->tile);
+                      a->tile, a->math, geom);
 }
 
 extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
@@ -922,6 +935,7 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
     if (rc) return rc;
     float* t = (float*)a->ws;
     p.bmat = w_dgrad;
+    p.bsplit = (const float*)a->w_split;
     p.M = (long)a->n * a->oh * a->ow;
     p.N = C;
     p.K = a->cout;
@@ -937,7 +951,7 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
     const bool vec16 = vec && (p.c1 % 16 == 0);
     hipStream_t st = as_stream(stream);
     rc = run_fwd_gemm(p, vec, vec16, a->tile, (char*)a->ws + tb, a->ws_bytes - tb, st,
-                      "pld_conv2d_dgrad");
+                      "pld_conv2d_dgrad", a->math);
     if (rc) return rc;
     const long total = (long)a->n * a->h * a->w * C;
     stride_scatter_kernel<<<std::min<unsigned>(cdiv(total, 256), 16384), 256, 0, st>>>(
@@ -966,6 +980,7 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   int rc = fill_geom(&g, p);
   if (rc) return rc;
   p.bmat = w_dgrad;
+  p.bsplit = (const float*)a->w_split;
   p.M = a->n * a->h * a->w;
   p.N = a->c1 + a->c2;
   p.K = a->kh * a->kw * a->cout;
@@ -980,27 +995,39 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   const bool vec = (p.c1 % 4 == 0) && aligned16(dy) && aligned16(w_dgrad);
   const bool vec16 = vec && (p.c1 % 16 == 0);
   return run_fwd_gemm(p, vec, vec16, a->tile, a->ws, a->ws_bytes, as_stream(stream),
-                      "pld_conv2d_dgrad");
+                      "pld_conv2d_dgrad", a->math);
 }
 
 static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& splits,
-                       int& kt_per, int& cfg) {
+                       int& kt_per, int& cfg, bool& x3) {
   M = a->kh * a->kw * (a->c1 + a->c2);
   N = a->cout;
   K = (long)a->n * a->oh * a->ow;
-  const long ktiles = (K + BK - 1) / BK;
-  // pick the tile for an unsplit GEMM, then split K until ~3 blocks per CU
-  cfg = choose_tile(M, N, K, 1, a->tile);
-  const long tiles = (long)cdiv(M, kTiles[cfg].bm) * cdiv(N, kTiles[cfg].bn);
-  long s = std::max<long>(1, (768 + tiles - 1) / tiles);
-  s = std::min<long>(s, std::max<long>(1, ktiles / 8));  // >= 8 k-steps per block
+  int tile;
+  resolve_sched(a->math, x3_wgrad_geom(a->c1, a->c2, a->cout), a->tile, x3, tile);
+  const int bk = x3 ? X3_BK : BK;
+  const long ktiles = (K + bk - 1) / bk;
+  // pick the tile for an unsplit GEMM, then split K until ~2-3 blocks per CU
+  int bm = 0, bn = 0;
+  if (x3) {
+    int tm, tn, occ;
+    cfg = x3_choose(M, N, K, tile, true);
+    pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+  } else {
+    cfg = choose_tile(M, N, K, 1, tile);
+    bm = kTiles[cfg].bm;
+    bn = kTiles[cfg].bn;
+  }
+  const long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
+  long s = std::max<long>(1, ((x3 ? 512 : 768) + tiles - 1) / tiles);
+  s = std::min<long>(s, std::max<long>(1, ktiles / (x3 ? 4 : 8)));  // >= 128 pixels per block
   // a workgroup's pixel range must stay within 32-bit buffer offsets of its base image
   const long img_in = (long)a->h * a->w * std::max(a->c1, a->c2) * 4;
   const long img_out = (long)a->oh * a->ow;
   for (;;) {
     const long kp = (ktiles + s - 1) / s;
-    const long span_a = (kp * BK / img_out + 2) * img_in;
-    const long span_b = kp * BK * (long)N * 4;
+    const long span_a = (kp * bk / img_out + 2) * img_in;
+    const long span_b = kp * bk * (long)N * 4;
     if ((span_a < MAX_RECORDS && span_b < MAX_RECORDS) || kp <= 1) break;
     ++s;
   }
@@ -1022,7 +1049,8 @@ extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
   if (pld__skinny_eligible(a)) return pld__skinny_wgrad_ws(a);
   int M, N, splits, kt, cfg;
   long K;
-  wgrad_plan(a, M, N, K, splits, kt, cfg);
+  bool x3;
+  wgrad_plan(a, M, N, K, splits, kt, cfg, x3);
   return wgrad_ws_bytes(splits, M, N);
 }
 
@@ -1040,7 +1068,8 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   }
   int M, N, splits, kt_per, cfg;
   long K;
-  wgrad_plan(a, M, N, K, splits, kt_per, cfg);
+  bool x3;
+  wgrad_plan(a, M, N, K, splits, kt_per, cfg, x3);
   PLD_CHECK_ARG(K < (1L << 31), "pld_conv2d_wgrad: too many pixels");
   const size_t need = wgrad_ws_bytes(splits, M, N);
   PLD_CHECK_ARG(ws_bytes >= need && (need == 0 || ws),
@@ -1067,7 +1096,12 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   const bool vec = (p.c1 % 4 == 0) && (p.c2 % 4 == 0) && aligned16(p.x1) &&
                    (!p.x2 || aligned16(p.x2)) && aligned16(dy) &&
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
-  rc = launch_igemm<MODE_WGRAD>(p, vec, false, splits, cfg, st);
+  if (x3) {
+    PLD_CHECK_ARG(vec, "pld_conv2d_wgrad: bf16x3 operands must be 16-byte aligned");
+    rc = pld__x3_launch(&p, MODE_WGRAD, splits, cfg, st);
+  } else {
+    rc = launch_igemm<MODE_WGRAD>(p, vec, false, splits, cfg, st);
+  }
   if (rc || splits == 1) return rc;
   const long n = (long)M * N;
   const float* src = (const float*)ws;

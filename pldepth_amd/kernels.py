@@ -6,6 +6,8 @@ computation is a call into libpldepth_hip.so. Nothing here falls back to torch m
 import ctypes as C
 import os
 
+import numpy as np
+
 import torch
 
 from ._lib import ConvArgs, lib
@@ -114,8 +116,34 @@ def same_pads(h, k, s):
     return total // 2, out
 
 
+# conv product arithmetic (pld_conv_args.math): "bf16x3" (fp32 via three bf16 MFMA products,
+# ~1e-5 relative per product) or "fp32" (exact fp32 MFMA). The model engines apply a policy:
+# "mixed" (default) runs the encoder's convs in fp32 and the decoder's in bf16x3 — the deep
+# training-mode-BN encoder chain amplifies per-op rounding at small batch sizes, while the decoder
+# holds ~83 % of the conv FLOPs; "bf16x3" / "fp32" use one arithmetic everywhere.
+# PLD_CONV_MATH overrides the default policy.
+MATH = {"fp32": 0, "bf16x3": 1}
+POLICIES = ("mixed", "bf16x3", "fp32")
+CONV_MATH = [os.environ.get("PLD_CONV_MATH", "mixed")]
+
+
+def set_conv_math(policy):
+    """Default conv policy for engines built afterwards (and for conv_args() without math=)."""
+    if policy not in POLICIES:
+        raise ValueError(f"conv math must be one of {POLICIES}, got {policy!r}")
+    CONV_MATH[0] = policy
+
+
+def conv_policy(policy=None):
+    """(encoder math, decoder math) of a policy (default: the current one)."""
+    policy = policy or CONV_MATH[0]
+    if policy not in POLICIES:
+        raise ValueError(f"conv math must be one of {POLICIES}, got {policy!r}")
+    return ("fp32", "bf16x3") if policy == "mixed" else (policy, policy)
+
+
 def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None, in_shift=None,
-              in_act="none"):
+              in_act="none", math=None):
     n, h, w, c1 = x1.shape
     c2 = 0 if x2 is None else x2.shape[3]
     a = ConvArgs()
@@ -130,6 +158,7 @@ def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None,
     a.in_shift = None if in_shift is None else in_shift.data_ptr()
     a.in_act = ACT[in_act]
     a.tile = -1
+    a.math = MATH[math or conv_policy()[1]]
     a._keep = (x1, x2, in_scale, in_shift)  # the struct holds raw pointers: keep owners alive
     return a
 
@@ -172,12 +201,26 @@ def save_tile_cache(path):
 
 def _shape_key(mode, a):
     return (mode, a.n, a.h, a.w, a.c1, a.c2, a.kh, a.kw, a.sh, a.sw, a.pad_t, a.pad_l, a.oh,
-            a.ow, a.cout, bool(a.in_scale))
+            a.ow, a.cout, bool(a.in_scale), a.math)
 
 
 def _skinny(a):
     return (a.cout == 1 and a.kh == 3 and a.kw == 3 and a.sh == 1 and a.c2 == 0
             and not a.in_scale and a.c1 % 4 == 0 and a.c1 <= 64)
+
+
+def _schedules(mode, math):
+    """Schedule indices worth timing (pld_conv_args.tile). fwd/dgrad: every tile x split-K
+    schedule; wgrad always sizes its own split, so only the tiles. Under bf16x3 the exact-fp32
+    schedules follow the bf16x3 ones."""
+    nf = lib().pld_conv_num_tiles()
+    n = lib().pld_conv_num_schedules(math)
+    if mode != "wgrad":
+        return list(range(n))
+    if n == nf:
+        return list(range(nf // 2))
+    nx = n - nf
+    return list(range(nx // 2)) + list(range(nx, nx + nf // 2))
 
 
 def _tune(mode, a, run):
@@ -190,8 +233,7 @@ def _tune(mode, a, run):
         return -1
     best, best_t = -1, float("inf")
     st = torch.cuda.current_stream()
-    n = lib().pld_conv_num_tiles()
-    for t in range(n // 2 if mode == "wgrad" else n):
+    for t in _schedules(mode, a.math):
         run(t)  # warm-up (also sizes the workspace)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
@@ -215,7 +257,29 @@ def _splitk_ws(args, fn):
         args.ws, args.ws_bytes = None, 0
 
 
+# bf16x3 pre-split copies of native/dgrad filters (pld_filter_split), keyed by the fp32 filter's
+# device address; the owner (engine_common._Conv.refresh) rewrites both together.
+_SPLIT = {}
+
+
+def filter_split(w, out=None):
+    """Split a [rows][K] fp32 filter (K % 8 == 0) for the bf16x3 kernel and register the copy
+    as the pre-split form of `w` for conv2d_fwd / conv2d_dgrad."""
+    out = torch.empty_like(w) if out is None else out
+    K_ = w.shape[-1] if w.dim() == 2 else int(np.prod(w.shape[1:]))
+    rows = w.shape[0]
+    lib().pld_filter_split(ptr(w), rows, K_, ptr(out), stream())
+    _SPLIT[w.data_ptr()] = out
+    return out
+
+
+def _set_split(args, w):
+    s = _SPLIT.get(w.data_ptr()) if args.math == MATH["bf16x3"] else None
+    args.w_split = None if s is None else s.data_ptr()
+
+
 def conv2d_fwd(args, w_native, bias, y, accumulate=False):
+    _set_split(args, w_native)
     if args.tile < 0:
         scratch = None
 
@@ -234,6 +298,7 @@ def conv2d_fwd(args, w_native, bias, y, accumulate=False):
 
 
 def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
+    _set_split(args, w_dgrad)
     if args.tile < 0:
         s1 = s2 = None
 

@@ -79,8 +79,11 @@ def same_pad(size, k, s):
 class EffNetFF:
     """Keras-named parameters + buffers + launch order of one ff_effnet replica."""
 
-    def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0):
+    def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0,
+                 conv_math=None):
         H, W, C = input_shape
+        # conv arithmetic per part (kernels.conv_policy): encoder / decoder
+        self.enc_math, self.dec_math = K.conv_policy(conv_math)
         assert C == 3 and H % 32 == 0 and W % 32 == 0, "input must be RGB with H, W % 32 == 0"
         self.H, self.W, self.B = H, W, batch_size
         self.device = torch.device(device)
@@ -288,7 +291,8 @@ class EffNetFF:
         pl, _ = correct_pad(self.W, 3)
         x = A["input"]
         h, w = self.H // 2, self.W // 2
-        args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none")
+        args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none",
+                 math=self.enc_math)
         K.conv2d_fwd(args, self.stem.w_nat, None, A["stem_pre"])
         rows = B * h * w
         self.stem_bn.stats_(A["stem_pre"], rows, training)
@@ -298,14 +302,15 @@ class EffNetFF:
             x = self._block_fwd(blk, x, training, step, li)
         h, w = x.shape[1], x.shape[2]
         rows = B * h * w
-        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280), self.top.w_nat, None, A["top_pre"])
+        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280, math=self.enc_math), self.top.w_nat,
+                     None, A["top_pre"])
         self.top_bn.stats_(A["top_pre"], rows, training)
         self.top_bn.apply(A["top_pre"], rows, "swish", A["top_activation"], training)
         x, x2 = A["top_activation"], None
         for i, (conv, bn, skip) in enumerate(self.dec):
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
-            args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout)
+            args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
             K.conv2d_fwd(args, conv.w_nat, conv.b, A[f"dec{i}_pre"])
             rows = B * h * w
             bn.stats_(A[f"dec{i}_pre"], rows, training)
@@ -315,15 +320,15 @@ class EffNetFF:
             x, x2 = A[f"dec{i}_up"], (A[skip] if skip else None)
         pt, _ = same_pad(h, 3, 1)
         pl, _ = same_pad(w, 3, 1)
-        K.conv2d_fwd(a(x, None, 3, 3, 1, pt, pl, h, w, 1), self.final.w_nat, self.final.b,
-                     A["pred"])
+        K.conv2d_fwd(a(x, None, 3, 3, 1, pt, pl, h, w, 1, math=self.dec_math), self.final.w_nat,
+                     self.final.b, A["pred"])
         return A["pred"]
 
     def _block_fwd(self, blk, x, training, step, li):
         A, B, n = self.act, self.B, blk["name"]
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
         if blk["ex"] != 1:
-            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"]),
+            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"], math=self.enc_math),
                          blk["expand"].w_nat, None, A[n + "expand_pre"])
             blk["expand_bn"].stats_(A[n + "expand_pre"], B * h * w, training)
             blk["expand_bn"].apply(A[n + "expand_pre"], B * h * w, "swish",
@@ -346,7 +351,8 @@ class EffNetFF:
                      hw=oh * ow)
         else:
             self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
-        K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"]),
+        K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
+                                 math=self.enc_math),
                      blk["project"].w_nat, None, A[n + "project_pre"])
         pbn = blk["project_bn"]
         pbn.stats_(A[n + "project_pre"], rows, training)
@@ -384,7 +390,7 @@ class EffNetFF:
         pt, _ = same_pad(h, 3, 1)
         pl, _ = same_pad(w, 3, 1)
         x4 = A["dec4_up"]
-        args = a(x4, None, 3, 3, 1, pt, pl, h, w, 1)
+        args = a(x4, None, 3, 3, 1, pt, pl, h, w, 1, math=self.dec_math)
         K.conv2d_wgrad(args, dpred, self.final.dw)
         K.channel_sum(dpred, B * h * w, 1, self.final.db)
         K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
@@ -404,7 +410,7 @@ class EffNetFF:
                 g1, g2 = G[f"dec{i - 1}_up"], (G[pskip] if pskip else None)
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
-            args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout)
+            args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
             K.conv2d_wgrad(args, gpre, conv.dw)
             K.channel_sum(gpre, rows, conv.cout, conv.db)
             K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
@@ -414,7 +420,8 @@ class EffNetFF:
         gpre = self._gpre_buf(A["top_pre"].shape)
         self.top_bn.bwd(A["top_pre"], G["top_activation"], rows, "swish", gpre)
         last = self.blocks[-1]["name"] + "output"
-        K.conv2d_dgrad(a(A[last], None, 1, 1, 1, 0, 0, h, w, 1280), gpre, self.top.w_dg, G[last])
+        K.conv2d_dgrad(a(A[last], None, 1, 1, 1, 0, 0, h, w, 1280, math=self.enc_math), gpre,
+                       self.top.w_dg, G[last])
         for bi in range(len(self.blocks) - 1, -1, -1):
             blk = self.blocks[bi]
             x_in = A[self.blocks[bi - 1]["name"] + "output"] if bi > 0 else A["stem_activation"]
@@ -440,7 +447,8 @@ class EffNetFF:
         gp = self._gpre_buf(A[n + "project_pre"].shape)
         blk["project_bn"].bwd(A[n + "project_pre"], gbn, rows, "none", gp)
         gse = G[n + "se_excite"]
-        K.conv2d_dgrad(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"]),
+        K.conv2d_dgrad(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
+                                   math=self.enc_math),
                        gp, blk["project"].w_dg, gse)
         F = self.frozen
         K.se_bwd(gse, A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
@@ -459,7 +467,8 @@ class EffNetFF:
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
             gpe = self._gpre_buf(A[n + "expand_pre"].shape)
             blk["expand_bn"].bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
-            K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"]), gpe,
+            K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
+                                       math=self.enc_math), gpe,
                            blk["expand"].w_dg, gx_in)
         else:
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)

@@ -138,8 +138,16 @@ class _Conv:
         self.w_nat = torch.empty(self.cout, self.k, self.k, self.cin, device=dev)
         self.w_dg = (torch.empty(self.cin, self.k, self.k, self.cout, device=dev)
                      if self.need_dgrad else None)
+        # bf16x3 pre-split copies (fwd K = k*k*cin, dgrad K = k*k*cout must be multiples of 8)
+        self.w_nat_x3 = torch.empty_like(self.w_nat) if self.cin % 8 == 0 else None
+        self.w_dg_x3 = (torch.empty_like(self.w_dg)
+                        if self.w_dg is not None and self.cout % 8 == 0 else None)
 
     def refresh(self):
         K.filter_to_native(self.w, self.w_nat)
+        if self.w_nat_x3 is not None:
+            K.filter_split(self.w_nat, self.w_nat_x3)
         if self.w_dg is not None:
             K.filter_to_dgrad(self.w, self.w_dg)
+            if self.w_dg_x3 is not None:
+                K.filter_split(self.w_dg, self.w_dg_x3)

@@ -48,8 +48,11 @@ def preprocess_input(x):
 class RedWebFF:
     """Keras-named parameters + buffers + launch order of one ff_redweb replica."""
 
-    def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0):
+    def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0,
+                 conv_math=None):
         H, W, C = input_shape
+        # conv arithmetic (kernels.conv_policy): frozen ResNet-50 encoder / trainable decoder
+        self.enc_math, self.dec_math = K.conv_policy(conv_math)
         assert C == 3 and H % 32 == 0 and W % 32 == 0, "input must be RGB with H, W % 32 == 0"
         self.H, self.W, self.B = H, W, batch_size
         self.device = torch.device(device)
@@ -228,6 +231,9 @@ class RedWebFF:
         return self._gpre[key]
 
     # ------------------------------------------------------------------ forward
+    def _math(self, conv):
+        return self.dec_math if conv.trainable else self.enc_math
+
     def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None):
         """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout]."""
         k, s = conv.k, conv.stride
@@ -235,7 +241,7 @@ class RedWebFF:
             pt, pl = (k - 1) // 2, (k - 1) // 2
         else:
             pt = pl = 0
-        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout)
+        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout, math=self._math(conv))
         K.conv2d_fwd(args, conv.w_nat, conv.b, y, accumulate=acc)
         return args
 
@@ -244,7 +250,7 @@ class RedWebFF:
         H, W = self.H, self.W
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
-        args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64)
+        args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64, math=self.enc_math)
         K.conv2d_fwd(args, self.stem.w_nat, self.stem.b, A["conv1_pre"])
         self.stem_bn.stats_(A["conv1_pre"], B * h * w, training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
@@ -328,7 +334,7 @@ class RedWebFF:
         """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given."""
         k, s = conv.k, conv.stride
         pt = pl = ((k - 1) // 2 if s == 1 else 0)
-        args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout)
+        args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout, math=self._math(conv))
         if conv.trainable:
             K.conv2d_wgrad(args, gy, conv.dw)
             if conv.db is not None:
