@@ -248,6 +248,14 @@ int pld_scale_per_sample(const float* x, const float* sample_scale, int n, int64
  * ------------------------------------------------------------------------------------------ */
 int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const float* wdw, int k, int s,
                    int pad_t, int pad_l, int oh, int ow, float* y, void* stream);
+/* forward with the producer's training-mode BN + activation fused into the input read:
+ * x' = act(((x - mean) * invstd) * gamma + beta) on in-image pixels (padding stays 0, as TF pads
+ * the activated tensor); the pre-activation tensor is read instead of a materialised
+ * activation (pl_hourglass.py:48 EfficientNet expand_bn -> expand_activation -> dwconv). */
+int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, const float* wdw, int k, int s,
+                      int pad_t, int pad_l, int oh, int ow, const float* mean,
+                      const float* invstd, const float* gamma, const float* beta, int act,
+                      float* y, void* stream);
 int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw, int k, int s,
                      int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
                      void* stream);
@@ -280,6 +288,8 @@ int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c, int cse, c
 size_t pld_sampler_workspace_size(int B, int H, int W, int R, int L, int strategy);
 int pld_sampler_compact(const float* mask, int B, int H, int W, const float* gt, int* valid_idx,
                         int* nvalid, float* gt_minmax, void* ws, void* stream);
+/* workspace of pld_sampler_compact (per-segment counts and gt min/max) */
+size_t pld_sampler_compact_workspace_size(int B, int H, int W);
 int pld_sampler_draw(const int* nvalid, int B, int n_cand, int L, uint64_t seed, uint64_t step,
                      int image_offset, int* draws, void* stream);
 /* graph-replayable form: the Philox step counter is read from step_dev[0] */

@@ -75,12 +75,15 @@ _SIGS = {
     "pld_dropconnect_scales": (I32, [P, I32, F32, U64, U64, I32, I32, P]),
     "pld_bn_inference_coeffs": (I32, [P, P, P, P, I32, F32, P, P, P]),
     "pld_dwconv_fwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
+    "pld_dwconv_fwd_bn": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P, P,
+                                P, I32, P, P]),
     "pld_dwconv_dgrad": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, I32, P]),
     "pld_se_workspace_size": (SZ, [I32, I32, I32, I32]),
     "pld_se_fwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
     "pld_se_bwd": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P]),
     "pld_sampler_workspace_size": (SZ, [I32, I32, I32, I32, I32, I32]),
     "pld_sampler_compact": (I32, [P, I32, I32, I32, P, P, P, P, P, P]),
+    "pld_sampler_compact_workspace_size": (SZ, [I32, I32, I32]),
     "pld_sampler_draw": (I32, [P, I32, I32, I32, U64, U64, I32, P, P]),
     "pld_sampler_rank": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, P, P]),
     "pld_sampler_candidates": (I32, [I32, I32]),
@@ -94,7 +97,8 @@ _SIGS = {
 _NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_num_schedules",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
-               "pld_sampler_workspace_size", "pld_sampler_candidates"}
+               "pld_sampler_workspace_size", "pld_sampler_candidates",
+               "pld_sampler_compact_workspace_size"}
 
 
 def declared_symbols(header=HEADER):

@@ -16,83 +16,182 @@
 
 namespace pld {
 
-template <int K>
-__global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ x, int n,
-                                                         int h, int w, int c,
-                                                         const float* __restrict__ wt, int s,
-                                                         int pt, int pl, int oh, int ow,
+// Index decomposition of a flat (img, row, column-tile, channel-quad) id with 32-bit magic
+// divisions (64-bit integer division is emulated and was the cost of the first version).
+struct DwGeom {
+  int n, h, w, c, oh, ow, s, pt, pl;
+  FastDiv dCV, dTiles, dRows;
+  const float* mean;  // optional input prologue: act(((x - mean) * invstd) * gamma + beta)
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+};
+
+__device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
+  acc.x += v.x * f.x;
+  acc.y += v.y * f.y;
+  acc.z += v.z * f.z;
+  acc.w += v.w * f.w;
+  return acc;
+}
+
+// forward: a thread owns T consecutive output columns of one row and 4 channels; the K rows of
+// its (T-1)S+K input columns are loaded once each (register window), instead of K*K per output.
+template <int K, int S, int T, bool PRO>
+__global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ wt, DwGeom g,
                                                          float* __restrict__ y) {
-  const int cv = c / 4;
-  const long total = (long)n * oh * ow * cv;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(e % cv);
-    long t = e / cv;
-    const int ox = (int)(t % ow);
-    t /= ow;
-    const int oy = (int)(t % oh);
-    const int img = (int)(t / oh);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* xb = x + (long)img * h * w * c + 4 * q;
+  constexpr int NC = (T - 1) * S + K;
+  const int cv = g.c / 4;
+  const int tiles = (g.ow + T - 1) / T;
+  const int total = g.n * g.oh * tiles * cv;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int t0 = (int)g.dCV.div((uint32_t)e);
+    const int q = e - t0 * cv;
+    const int t1 = (int)g.dTiles.div((uint32_t)t0);
+    const int ox0 = (t0 - t1 * tiles) * T;
+    const int img = (int)g.dRows.div((uint32_t)t1);
+    const int oy = t1 - img * g.oh;
+    float4 mu, is, ga, be;
+    if (PRO) {
+      mu = *reinterpret_cast<const float4*>(g.mean + 4 * q);
+      is = *reinterpret_cast<const float4*>(g.invstd + 4 * q);
+      ga = *reinterpret_cast<const float4*>(g.gamma + 4 * q);
+      be = *reinterpret_cast<const float4*>(g.beta + 4 * q);
+    }
+    float4 acc[T];
+#pragma unroll
+    for (int o = 0; o < T; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* xb = x + (long)img * g.h * g.w * g.c + 4 * q;
+    const int ix0 = ox0 * S - g.pl;
 #pragma unroll
     for (int ty = 0; ty < K; ++ty) {
-      const int iy = oy * s + ty - pt;
-      if (iy < 0 || iy >= h) continue;
+      const int iy = oy * S + ty - g.pt;
+      if (iy < 0 || iy >= g.h) continue;
+      float4 row[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int ix = ix0 + j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ix >= 0 && ix < g.w) {
+          v = *reinterpret_cast<const float4*>(xb + ((long)iy * g.w + ix) * g.c);
+          if (PRO) {  // the bn_apply arithmetic, then the activation (TF pads the activated map)
+            v = make_float4(act_fwd(g.act, ((v.x - mu.x) * is.x) * ga.x + be.x),
+                            act_fwd(g.act, ((v.y - mu.y) * is.y) * ga.y + be.y),
+                            act_fwd(g.act, ((v.z - mu.z) * is.z) * ga.z + be.z),
+                            act_fwd(g.act, ((v.w - mu.w) * is.w) * ga.w + be.w));
+          }
+        }
+        row[j] = v;
+      }
 #pragma unroll
       for (int tx = 0; tx < K; ++tx) {
-        const int ix = ox * s + tx - pl;
-        if (ix < 0 || ix >= w) continue;
-        const float4 v = *reinterpret_cast<const float4*>(xb + ((long)iy * w + ix) * c);
-        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * c + 4 * q);
-        acc.x += v.x * f.x;
-        acc.y += v.y * f.y;
-        acc.z += v.z * f.z;
-        acc.w += v.w * f.w;
+        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
+#pragma unroll
+        for (int o = 0; o < T; ++o) acc[o] = fma4(acc[o], row[o * S + tx], f);
       }
     }
-    *reinterpret_cast<float4*>(y + e * 4) = acc;
+    float* yb = y + (((long)img * g.oh + oy) * g.ow) * g.c + 4 * q;
+#pragma unroll
+    for (int o = 0; o < T; ++o)
+      if (ox0 + o < g.ow) *reinterpret_cast<float4*>(yb + (long)(ox0 + o) * g.c) = acc[o];
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restrict__ dy, int n,
-                                                           int h, int w, int c,
-                                                           const float* __restrict__ wt, int s,
-                                                           int pt, int pl, int oh, int ow,
-                                                           float* __restrict__ dx, int accum) {
-  const int cv = c / 4;
-  const long total = (long)n * h * w * cv;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(e % cv);
-    long t = e / cv;
-    const int ix = (int)(t % w);
-    t /= w;
-    const int iy = (int)(t % h);
-    const int img = (int)(t / h);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* db = dy + (long)img * oh * ow * c + 4 * q;
+// input gradient, stride 1: dx[iy][ix] = sum dy[iy+pt-ty][ix+pl-tx] w[ty][tx]; T columns per
+// thread from a T+K-1 column window of dy
+template <int K, int T>
+__global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __restrict__ dy,
+                                                              const float* __restrict__ wt,
+                                                              DwGeom g, float* __restrict__ dx,
+                                                              int accum) {
+  constexpr int NC = T + K - 1;
+  const int cv = g.c / 4;
+  const int tiles = (g.w + T - 1) / T;
+  const int total = g.n * g.h * tiles * cv;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int t0 = (int)g.dCV.div((uint32_t)e);
+    const int q = e - t0 * cv;
+    const int t1 = (int)g.dTiles.div((uint32_t)t0);
+    const int ix0 = (t0 - t1 * tiles) * T;
+    const int img = (int)g.dRows.div((uint32_t)t1);
+    const int iy = t1 - img * g.h;
+    float4 acc[T];
+#pragma unroll
+    for (int o = 0; o < T; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* db = dy + (long)img * g.oh * g.ow * g.c + 4 * q;
+    const int ox_lo = ix0 + g.pl - (K - 1);
 #pragma unroll
     for (int ty = 0; ty < K; ++ty) {
-      const int ny = iy + pt - ty;
-      if (ny < 0 || ny % s) continue;
-      const int oy = ny / s;
-      if (oy >= oh) continue;
+      const int oy = iy + g.pt - ty;
+      if (oy < 0 || oy >= g.oh) continue;
+      float4 row[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int ox = ox_lo + j;
+        row[j] = (ox >= 0 && ox < g.ow)
+                     ? *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
       for (int tx = 0; tx < K; ++tx) {
-        const int nx = ix + pl - tx;
-        if (nx < 0 || nx % s) continue;
-        const int ox = nx / s;
-        if (ox >= ow) continue;
-        const float4 v = *reinterpret_cast<const float4*>(db + ((long)oy * ow + ox) * c);
-        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * c + 4 * q);
-        acc.x += v.x * f.x;
-        acc.y += v.y * f.y;
-        acc.z += v.z * f.z;
-        acc.w += v.w * f.w;
+        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
+        // output o uses dy column ix0 + o + pl - tx = ox_lo + (o + K - 1 - tx)
+#pragma unroll
+        for (int o = 0; o < T; ++o) acc[o] = fma4(acc[o], row[o + K - 1 - tx], f);
       }
     }
-    float4* d = reinterpret_cast<float4*>(dx + e * 4);
+    float* xb = dx + (((long)img * g.h + iy) * g.w) * g.c + 4 * q;
+#pragma unroll
+    for (int o = 0; o < T; ++o) {
+      if (ix0 + o >= g.w) continue;
+      float4* d = reinterpret_cast<float4*>(xb + (long)(ix0 + o) * g.c);
+      float4 v = acc[o];
+      if (accum) {
+        const float4 old = *d;
+        v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+      }
+      *d = v;
+    }
+  }
+}
+
+// input gradient, any stride: one output pixel per thread, taps of matching parity only
+template <int K>
+__global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restrict__ dy,
+                                                           const float* __restrict__ wt,
+                                                           DwGeom g, float* __restrict__ dx,
+                                                           int accum) {
+  const int cv = g.c / 4;
+  const int total = g.n * g.h * g.w * cv;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int t0 = (int)g.dCV.div((uint32_t)e);
+    const int q = e - t0 * cv;
+    const int t1 = (int)g.dTiles.div((uint32_t)t0);  // tiles == w here
+    const int ix = t0 - t1 * g.w;
+    const int img = (int)g.dRows.div((uint32_t)t1);
+    const int iy = t1 - img * g.h;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* db = dy + (long)img * g.oh * g.ow * g.c + 4 * q;
+#pragma unroll
+    for (int ty = 0; ty < K; ++ty) {
+      const int ny = iy + g.pt - ty;
+      if (ny < 0 || ny % g.s) continue;
+      const int oy = ny / g.s;
+      if (oy >= g.oh) continue;
+#pragma unroll
+      for (int tx = 0; tx < K; ++tx) {
+        const int nx = ix + g.pl - tx;
+        if (nx < 0 || nx % g.s) continue;
+        const int ox = nx / g.s;
+        if (ox >= g.ow) continue;
+        const float4 v = *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c);
+        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
+        acc = fma4(acc, v, f);
+      }
+    }
+    float4* d = reinterpret_cast<float4*>(dx + (long)e * 4);
     if (accum) {
       const float4 o = *d;
       acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
@@ -147,79 +246,125 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
 }
 
 // forward excitation, one workgroup per image
-__global__ __launch_bounds__(256) void se_fc_fwd_kernel(const double* __restrict__ part,
-                                                        int rsplit, int hw, int c, int cse,
-                                                        const float* __restrict__ w1,
-                                                        const float* __restrict__ b1,
-                                                        const float* __restrict__ w2,
-                                                        const float* __restrict__ b2,
-                                                        float* __restrict__ pooled,
-                                                        float* __restrict__ z1,
-                                                        float* __restrict__ gate) {
+// SE excitation FCs (tiny: c <= 1152, cse <= 48 per image). Grid (image, SE_SLICES) of
+// 1024-thread workgroups: every workgroup rebuilds the image's full hidden vector (z1 fwd /
+// dz1 bwd) with short dependency chains (16 channel slices x 64 hidden lanes, then a fixed-order
+// LDS combine) and writes its own slice of the c outputs. Workgroup 0 of an image also stores
+// pooled and z1 (the backward needs z1).
+constexpr int SE_SLICES = 8;
+constexpr int SE_THREADS = 1024;
+constexpr int SE_CS = SE_THREADS / 64;  // channel slices
+
+// out[j] = sum_ch v[ch] * w[ch * cse + j] (w row-major [c][cse]; lanes over j: coalesced)
+__device__ __forceinline__ void se_vecmat_cj(const float* v, const float* __restrict__ w, int c,
+                                             int cse, float* red /* [SE_THREADS] */,
+                                             float* out) {
+  const int jl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  for (int j0 = 0; j0 < cse; j0 += 64) {
+    const int j = j0 + jl;
+    float a0 = 0.f, a1 = 0.f;
+    if (j < cse) {
+      int ch = sl;
+      for (; ch + SE_CS < c; ch += 2 * SE_CS) {
+        a0 += v[ch] * w[(long)ch * cse + j];
+        a1 += v[ch + SE_CS] * w[(long)(ch + SE_CS) * cse + j];
+      }
+      if (ch < c) a0 += v[ch] * w[(long)ch * cse + j];
+    }
+    red[threadIdx.x] = a0 + a1;
+    __syncthreads();
+    if (sl == 0 && j < cse) {
+      float t = red[jl];
+      for (int k = 1; k < SE_CS; ++k) t += red[k * 64 + jl];
+      out[j] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// out[j] = sum_ch v[ch] * w[j * c + ch] (w row-major [cse][c]): one wave per j, lanes over ch
+__device__ __forceinline__ void se_vecmat_jc(const float* v, const float* __restrict__ w, int c,
+                                             int cse, float* out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int j = wave; j < cse; j += SE_THREADS / 64) {
+    float acc = 0.f;
+    for (int ch = lane; ch < c; ch += 64) acc += v[ch] * w[(long)j * c + ch];
+    acc = wave_sum(acc);
+    if (lane == 0) out[j] = acc;
+  }
+}
+
+__global__ __launch_bounds__(SE_THREADS) void se_fc_fwd_kernel(const double* __restrict__ part,
+                                                               int rsplit, int hw, int c, int cse,
+                                                               const float* __restrict__ w1,
+                                                               const float* __restrict__ b1,
+                                                               const float* __restrict__ w2,
+                                                               const float* __restrict__ b2,
+                                                               float* __restrict__ pooled,
+                                                               float* __restrict__ z1,
+                                                               float* __restrict__ gate) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sp = sm;          // [c] pooled
-  float* sh = sm + c;      // [cse] swish(z1)
-  const int img = blockIdx.x;
-  for (int ch = threadIdx.x; ch < c; ch += 256) {
+  float* sp = sm;             // [c] pooled
+  float* sh = sm + c;         // [cse] z1 - b1, then swish(z1)
+  float* red = sh + cse;      // [SE_THREADS]
+  const int img = blockIdx.x, slice = blockIdx.y;
+  for (int ch = threadIdx.x; ch < c; ch += SE_THREADS) {
     double s = 0.0;
     for (int k = 0; k < rsplit; ++k) s += part[((long)img * rsplit + k) * c + ch];
-    const float m = (float)(s / (double)hw);
-    sp[ch] = m;
-    pooled[(long)img * c + ch] = m;
+    sp[ch] = (float)(s / (double)hw);
   }
   __syncthreads();
-  // z1[j] = sum_c pooled[c] w1[c][j] + b1[j]: one wave per j (round robin)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j = wave; j < cse; j += 4) {
-    float acc = 0.f;
-    for (int ch = lane; ch < c; ch += 64) acc += sp[ch] * w1[(long)ch * cse + j];
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      const float z = acc + b1[j];
-      z1[(long)img * cse + j] = z;
-      sh[j] = z * sigmoidf_(z);
-    }
+  se_vecmat_cj(sp, w1, c, cse, red, sh);
+  if ((int)threadIdx.x < cse) {
+    const int j = threadIdx.x;
+    const float z = sh[j] + b1[j];
+    if (slice == 0) z1[(long)img * cse + j] = z;
+    sh[j] = z * sigmoidf_(z);
   }
+  if (slice == 0)
+    for (int ch = threadIdx.x; ch < c; ch += SE_THREADS) pooled[(long)img * c + ch] = sp[ch];
   __syncthreads();
-  for (int ch = threadIdx.x; ch < c; ch += 256) {
+  const int per = (c + SE_SLICES - 1) / SE_SLICES;
+  const int cb = slice * per, ce = min(c, cb + per);
+  for (int ch = cb + threadIdx.x; ch < ce; ch += SE_THREADS) {
     float acc = b2[ch];
     for (int j = 0; j < cse; ++j) acc += sh[j] * w2[(long)j * c + ch];
     gate[(long)img * c + ch] = sigmoidf_(acc);
   }
 }
 
-// backward through the excitation: addn = (d pooled) / hw
-__global__ __launch_bounds__(256) void se_fc_bwd_kernel(const double* __restrict__ part,
-                                                        int rsplit, int hw, int c, int cse,
-                                                        const float* __restrict__ w1,
-                                                        const float* __restrict__ w2,
-                                                        const float* __restrict__ z1,
-                                                        const float* __restrict__ gate,
-                                                        float* __restrict__ addn) {
+// SE backward: given S[c] = sum_hw dy*a (squeeze partials of the product), dz2 = S g (1-g),
+// dz1 = (w2 . dz2) swish'(z1), addn[c] = (w1 . dz1)[c] / hw.
+__global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __restrict__ part,
+                                                               int rsplit, int hw, int c, int cse,
+                                                               const float* __restrict__ w1,
+                                                               const float* __restrict__ w2,
+                                                               const float* __restrict__ z1,
+                                                               const float* __restrict__ gate,
+                                                               float* __restrict__ addn) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dz2 = sm;       // [c]
   float* dz1 = sm + c;   // [cse]
-  const int img = blockIdx.x;
-  for (int ch = threadIdx.x; ch < c; ch += 256) {
+  const int img = blockIdx.x, slice = blockIdx.y;
+  for (int ch = threadIdx.x; ch < c; ch += SE_THREADS) {
     double s = 0.0;
     for (int k = 0; k < rsplit; ++k) s += part[((long)img * rsplit + k) * c + ch];
     const float g = gate[(long)img * c + ch];
     dz2[ch] = (float)s * g * (1.f - g);
   }
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j = wave; j < cse; j += 4) {
-    float acc = 0.f;
-    for (int ch = lane; ch < c; ch += 64) acc += dz2[ch] * w2[(long)j * c + ch];
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      const float z = z1[(long)img * cse + j];
-      const float sg = sigmoidf_(z);
-      dz1[j] = acc * (sg * (1.f + z * (1.f - sg)));
-    }
+  se_vecmat_jc(dz2, w2, c, cse, dz1);
+  __syncthreads();
+  if ((int)threadIdx.x < cse) {
+    const int j = threadIdx.x;
+    const float z = z1[(long)img * cse + j];
+    const float sg = sigmoidf_(z);
+    dz1[j] *= sg * (1.f + z * (1.f - sg));
   }
   __syncthreads();
-  for (int ch = threadIdx.x; ch < c; ch += 256) {
+  const int per = (c + SE_SLICES - 1) / SE_SLICES;
+  const int cb = slice * per, ce = min(c, cb + per);
+  for (int ch = cb + threadIdx.x; ch < ce; ch += SE_THREADS) {
     float acc = 0.f;
     for (int j = 0; j < cse; ++j) acc += dz1[j] * w1[(long)ch * cse + j];
     addn[(long)img * c + ch] = acc / (float)hw;
@@ -239,20 +384,52 @@ static int se_rsplit(int n, int hw, int c) {
 
 using namespace pld;
 
-extern "C" int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const float* wdw, int k,
-                              int s, int pad_t, int pad_l, int oh, int ow, float* y,
-                              void* stream) {
+static DwGeom dw_geom(int n, int h, int w, int c, int s, int pt, int pl, int oh, int ow) {
+  DwGeom g{};
+  g.n = n; g.h = h; g.w = w; g.c = c; g.s = s; g.pt = pt; g.pl = pl; g.oh = oh; g.ow = ow;
+  g.dCV = FastDiv((uint32_t)(c / 4));
+  return g;
+}
+
+template <int K, int S, int T>
+static void dw_fwd_launch(const float* x, const float* wdw, DwGeom& g, float* y, hipStream_t st) {
+  g.dTiles = FastDiv((uint32_t)((g.ow + T - 1) / T));
+  g.dRows = FastDiv((uint32_t)g.oh);
+  const long total = (long)g.n * g.oh * ((g.ow + T - 1) / T) * (g.c / 4);
+  if (g.mean) dwconv_fwd_kernel<K, S, T, true><<<grid_for(total), 256, 0, st>>>(x, wdw, g, y);
+  else dwconv_fwd_kernel<K, S, T, false><<<grid_for(total), 256, 0, st>>>(x, wdw, g, y);
+}
+
+extern "C" int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, const float* wdw,
+                                 int k, int s, int pad_t, int pad_l, int oh, int ow,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, float* y, void* stream) {
   PLD_CHECK_ARG(x && wdw && y && n > 0 && h > 0 && w > 0 && c > 0 && s > 0 && oh > 0 && ow > 0,
                 "pld_dwconv_fwd: bad args");
   PLD_CHECK_ARG(c % 4 == 0, "pld_dwconv_fwd: channels must be a multiple of 4");
-  const long total = (long)n * oh * ow * (c / 4);
+  PLD_CHECK_ARG(!mean || (invstd && gamma && beta), "pld_dwconv_fwd_bn: incomplete BN prologue");
+  PLD_CHECK_ARG((long)n * h * w * c < (1L << 31) && (long)n * oh * ow * c < (1L << 31),
+                "pld_dwconv_fwd: tensor too large for 32-bit indexing");
+  PLD_CHECK_ARG(s == 1 || s == 2, "pld_dwconv_fwd: stride %d unsupported (1, 2)", s);
+  DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
+  g.mean = mean; g.invstd = invstd; g.gamma = gamma; g.beta = beta; g.act = act;
   hipStream_t st = as_stream(stream);
-  switch (k) {
-    case 3: dwconv_fwd_kernel<3><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, wdw, s, pad_t, pad_l, oh, ow, y); break;
-    case 5: dwconv_fwd_kernel<5><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, wdw, s, pad_t, pad_l, oh, ow, y); break;
-    default: set_error("pld_dwconv_fwd: kernel size %d unsupported (3, 5)", k); return PLD_ERR_UNSUPPORTED;
+  if (k == 3 && s == 1) dw_fwd_launch<3, 1, 4>(x, wdw, g, y, st);
+  else if (k == 3) dw_fwd_launch<3, 2, 2>(x, wdw, g, y, st);
+  else if (k == 5 && s == 1) dw_fwd_launch<5, 1, 4>(x, wdw, g, y, st);
+  else if (k == 5) dw_fwd_launch<5, 2, 2>(x, wdw, g, y, st);
+  else {
+    set_error("pld_dwconv_fwd: kernel size %d unsupported (3, 5)", k);
+    return PLD_ERR_UNSUPPORTED;
   }
   return check_launch("dwconv_fwd_kernel");
+}
+
+extern "C" int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const float* wdw, int k,
+                              int s, int pad_t, int pad_l, int oh, int ow, float* y,
+                              void* stream) {
+  return pld_dwconv_fwd_bn(x, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, nullptr, nullptr,
+                           nullptr, nullptr, 0, y, stream);
 }
 
 extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw,
@@ -261,12 +438,25 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
   PLD_CHECK_ARG(dy && wdw && dx && n > 0 && h > 0 && w > 0 && c > 0 && s > 0 && oh > 0 && ow > 0,
                 "pld_dwconv_dgrad: bad args");
   PLD_CHECK_ARG(c % 4 == 0, "pld_dwconv_dgrad: channels must be a multiple of 4");
-  const long total = (long)n * h * w * (c / 4);
+  PLD_CHECK_ARG((long)n * h * w * c < (1L << 31) && (long)n * oh * ow * c < (1L << 31),
+                "pld_dwconv_dgrad: tensor too large for 32-bit indexing");
+  PLD_CHECK_ARG(k == 3 || k == 5, "pld_dwconv_dgrad: kernel size %d unsupported (3, 5)", k);
+  DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
+  g.dRows = FastDiv((uint32_t)h);
   hipStream_t st = as_stream(stream);
-  switch (k) {
-    case 3: dwconv_dgrad_kernel<3><<<grid_for(total), 256, 0, st>>>(dy, n, h, w, c, wdw, s, pad_t, pad_l, oh, ow, dx, accumulate); break;
-    case 5: dwconv_dgrad_kernel<5><<<grid_for(total), 256, 0, st>>>(dy, n, h, w, c, wdw, s, pad_t, pad_l, oh, ow, dx, accumulate); break;
-    default: set_error("pld_dwconv_dgrad: kernel size %d unsupported (3, 5)", k); return PLD_ERR_UNSUPPORTED;
+  if (s == 1) {
+    constexpr int T = 4;
+    g.dTiles = FastDiv((uint32_t)((w + T - 1) / T));
+    const long total = (long)n * h * ((w + T - 1) / T) * (c / 4);
+    if (k == 3)
+      dwconv_dgrad_s1_kernel<3, T><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    else
+      dwconv_dgrad_s1_kernel<5, T><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+  } else {
+    g.dTiles = FastDiv((uint32_t)w);
+    const long total = (long)n * h * w * (c / 4);
+    if (k == 3) dwconv_dgrad_kernel<3><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    else dwconv_dgrad_kernel<5><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
   }
   return check_launch("dwconv_dgrad_kernel");
 }
@@ -289,7 +479,7 @@ extern "C" int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const f
   img_chan_sum_kernel<<<g1, 256, 0, st>>>(a, nullptr, hw, c, rs, (double*)ws);
   int rc = check_launch("img_chan_sum_kernel");
   if (rc) return rc;
-  se_fc_fwd_kernel<<<n, 256, sizeof(float) * (c + cse), st>>>(
+  se_fc_fwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse + SE_THREADS), st>>>(
       (const double*)ws, rs, hw, c, cse, w1, b1, w2, b2, pooled, z1, gate);
   return check_launch("se_fc_fwd_kernel");
 }
@@ -307,7 +497,7 @@ extern "C" int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c,
   img_chan_sum_kernel<<<g1, 256, 0, st>>>(a, dy, hw, c, rs, (double*)ws);
   int rc = check_launch("img_chan_sum_kernel(bwd)");
   if (rc) return rc;
-  se_fc_bwd_kernel<<<n, 256, sizeof(float) * (c + cse), st>>>((const double*)ws, rs, hw, c, cse,
-                                                               w1, w2, z1, gate, addn);
+  se_fc_bwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse), st>>>(
+      (const double*)ws, rs, hw, c, cse, w1, w2, z1, gate, addn);
   return check_launch("se_fc_bwd_kernel");
 }

@@ -18,25 +18,40 @@
 
 namespace pld {
 
-constexpr int SAMPLER_COMPACT_THREADS = 1024;
-
 // ------------------------------------------------------------------ compaction + min/max
-__global__ __launch_bounds__(1024) void compact_kernel(const float* __restrict__ mask, int HW,
-                                                       const float* __restrict__ gt,
-                                                       int* __restrict__ valid_idx,
-                                                       int* __restrict__ nvalid,
-                                                       float* __restrict__ gt_minmax) {
-  __shared__ int s_cnt[SAMPLER_COMPACT_THREADS];
-  __shared__ float s_min[SAMPLER_COMPACT_THREADS], s_max[SAMPLER_COMPACT_THREADS];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int chunk = (HW + SAMPLER_COMPACT_THREADS - 1) / SAMPLER_COMPACT_THREADS;
-  const int beg = min(HW, tid * chunk), end = min(HW, beg + chunk);
+// np.where(mask > 0) order (row-major flat index, sampling.py:135) for every image, plus the
+// whole-image gt min/max of the Info strategy (sampling.py:223). Images are cut into segments of
+// COMPACT_SEG pixels: pass 1 counts each segment's valid pixels (and its gt min/max), pass 2
+// gives each segment its output offset (sum of the earlier segments' counts) and writes its
+// indices in order with wave-ballot prefix sums. Reads are coalesced; 2 x B x S workgroups.
+constexpr int COMPACT_THREADS = 1024;
+constexpr int COMPACT_SEG = 16384;
+
+__device__ __forceinline__ int block_sum_1024(int v, int* s_w) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) s_w[w] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int i = 0; i < COMPACT_THREADS / 64; ++i) t += s_w[i];
+  return t;
+}
+
+__global__ __launch_bounds__(COMPACT_THREADS) void compact_count_kernel(
+    const float* __restrict__ mask, int HW, const float* __restrict__ gt, int S,
+    int* __restrict__ seg_cnt, float* __restrict__ seg_mm) {
+  __shared__ int s_w[COMPACT_THREADS / 64];
+  __shared__ float s_mn[COMPACT_THREADS / 64], s_mx[COMPACT_THREADS / 64];
+  const int s = blockIdx.x, b = blockIdx.y;
+  const int beg = s * COMPACT_SEG, end = min(HW, beg + COMPACT_SEG);
   const float* mb = mask + (long)b * HW;
   const float* gb = gt ? gt + (long)b * HW : nullptr;
   int cnt = 0;
   float mn = INFINITY, mx = -INFINITY;
-  for (int i = beg; i < end; ++i) {
+  for (int i = beg + threadIdx.x; i < end; i += COMPACT_THREADS) {
     cnt += mb[i] > 0.f;
     if (gb) {
       const float g = gb[i];
@@ -44,32 +59,72 @@ __global__ __launch_bounds__(1024) void compact_kernel(const float* __restrict__
       mx = fmaxf(mx, g);
     }
   }
-  s_cnt[tid] = cnt;
-  s_min[tid] = mn;
-  s_max[tid] = mx;
+  const int tot = block_sum_1024(cnt, s_w);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  }
+  if (lane == 0) {
+    s_mn[w] = mn;
+    s_mx[w] = mx;
+  }
   __syncthreads();
-  // inclusive Hillis-Steele scan over counts; min/max tree reduction
-  for (int o = 1; o < SAMPLER_COMPACT_THREADS; o <<= 1) {
-    const int v = tid >= o ? s_cnt[tid - o] : 0;
-    __syncthreads();
-    s_cnt[tid] += v;
-    __syncthreads();
-  }
-  for (int s = SAMPLER_COMPACT_THREADS / 2; s > 0; s >>= 1) {
-    if (tid < s) {
-      s_min[tid] = fminf(s_min[tid], s_min[tid + s]);
-      s_max[tid] = fmaxf(s_max[tid], s_max[tid + s]);
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < COMPACT_THREADS / 64; ++i) {
+      mn = fminf(mn, s_mn[i]);
+      mx = fmaxf(mx, s_mx[i]);
     }
-    __syncthreads();
+    seg_cnt[b * S + s] = tot;
+    seg_mm[2 * (b * S + s)] = mn;
+    seg_mm[2 * (b * S + s) + 1] = mx;
   }
-  int pos = s_cnt[tid] - cnt;
+}
+
+__global__ __launch_bounds__(COMPACT_THREADS) void compact_write_kernel(
+    const float* __restrict__ mask, int HW, int S, const int* __restrict__ seg_cnt,
+    const float* __restrict__ seg_mm, int* __restrict__ valid_idx, int* __restrict__ nvalid,
+    float* __restrict__ gt_minmax) {
+  __shared__ int s_w[COMPACT_THREADS / 64];
+  const int s = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int off = 0;
+  for (int i = 0; i < s; ++i) off += seg_cnt[b * S + i];
+  if (s == 0 && threadIdx.x == 0) {
+    int n = 0;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int i = 0; i < S; ++i) {
+      n += seg_cnt[b * S + i];
+      mn = fminf(mn, seg_mm[2 * (b * S + i)]);
+      mx = fmaxf(mx, seg_mm[2 * (b * S + i) + 1]);
+    }
+    nvalid[b] = n;
+    if (gt_minmax) {
+      gt_minmax[2 * b] = mn;
+      gt_minmax[2 * b + 1] = mx;
+    }
+  }
+  const int beg = s * COMPACT_SEG, end = min(HW, beg + COMPACT_SEG);
+  const float* mb = mask + (long)b * HW;
   int* out = valid_idx + (long)b * HW;
-  for (int i = beg; i < end; ++i)
-    if (mb[i] > 0.f) out[pos++] = i;
-  if (tid == SAMPLER_COMPACT_THREADS - 1) nvalid[b] = s_cnt[tid];
-  if (tid == 0 && gt_minmax) {
-    gt_minmax[2 * b] = s_min[0];
-    gt_minmax[2 * b + 1] = s_max[0];
+  for (int base = beg; base < end; base += COMPACT_THREADS) {
+    const int i = base + threadIdx.x;
+    const bool f = i < end && mb[i] > 0.f;
+    const unsigned long long bal = __ballot(f);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    __syncthreads();  // s_w reuse
+    if (lane == 0) s_w[w] = __popcll(bal);
+    __syncthreads();
+    int wave_off = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < COMPACT_THREADS / 64; ++k) {
+      const int c = s_w[k];
+      wave_off += k < w ? c : 0;
+      total += c;
+    }
+    if (f) out[off + wave_off + before] = i;
+    off += total;
   }
 }
 
@@ -294,9 +349,24 @@ extern "C" int pld_sampler_compact(const float* mask, int B, int H, int W, const
                 "pld_sampler_compact: bad args");
   PLD_CHECK_ARG((long)H * W < (1 << 24), "pld_sampler_compact: H*W must stay below 2^24 "
                 "(flat indices travel as float32)");
-  compact_kernel<<<B, SAMPLER_COMPACT_THREADS, 0, as_stream(stream)>>>(mask, H * W, gt, valid_idx,
-                                                                      nvalid, gt_minmax);
-  return check_launch("compact_kernel");
+  const int HW = H * W;
+  const int S = (int)cdiv(HW, COMPACT_SEG);
+  PLD_CHECK_ARG(ws, "pld_sampler_compact: workspace required (pld_sampler_compact_workspace_size)");
+  int* seg_cnt = (int*)ws;
+  float* seg_mm = (float*)((char*)ws + align_up(sizeof(int) * (size_t)B * S));
+  hipStream_t st = as_stream(stream);
+  compact_count_kernel<<<dim3(S, B), COMPACT_THREADS, 0, st>>>(mask, HW, gt, S, seg_cnt, seg_mm);
+  int rc = check_launch("compact_count_kernel");
+  if (rc) return rc;
+  compact_write_kernel<<<dim3(S, B), COMPACT_THREADS, 0, st>>>(mask, HW, S, seg_cnt, seg_mm,
+                                                               valid_idx, nvalid, gt_minmax);
+  return check_launch("compact_write_kernel");
+}
+
+extern "C" size_t pld_sampler_compact_workspace_size(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  const size_t S = cdiv((long)H * W, COMPACT_SEG);
+  return align_up(sizeof(int) * B * S) + align_up(2 * sizeof(float) * B * S);
 }
 
 extern "C" int pld_sampler_draw(const int* nvalid, int B, int n_cand, int L, uint64_t seed,

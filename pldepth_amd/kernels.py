@@ -257,24 +257,20 @@ def _splitk_ws(args, fn):
         args.ws, args.ws_bytes = None, 0
 
 
-# bf16x3 pre-split copies of native/dgrad filters (pld_filter_split), keyed by the fp32 filter's
-# device address; the owner (engine_common._Conv.refresh) rewrites both together.
-_SPLIT = {}
-
-
 def filter_split(w, out=None):
-    """Split a [rows][K] fp32 filter (K % 8 == 0) for the bf16x3 kernel and register the copy
-    as the pre-split form of `w` for conv2d_fwd / conv2d_dgrad."""
+    """Split a [rows][K] fp32 filter (K % 8 == 0) for the bf16x3 kernel and attach the copy to
+    the fp32 tensor object (w._pld_split): conv2d_fwd / conv2d_dgrad given that same tensor use
+    it. The owner (engine_common._Conv.refresh) rewrites both together."""
     out = torch.empty_like(w) if out is None else out
     K_ = w.shape[-1] if w.dim() == 2 else int(np.prod(w.shape[1:]))
     rows = w.shape[0]
     lib().pld_filter_split(ptr(w), rows, K_, ptr(out), stream())
-    _SPLIT[w.data_ptr()] = out
+    w._pld_split = out
     return out
 
 
 def _set_split(args, w):
-    s = _SPLIT.get(w.data_ptr()) if args.math == MATH["bf16x3"] else None
+    s = getattr(w, "_pld_split", None) if args.math == MATH["bf16x3"] else None
     args.w_split = None if s is None else s.data_ptr()
 
 
@@ -436,11 +432,19 @@ def scale_per_sample(x, sample_scale, y, accumulate=False):
 
 
 # ------------------------------------------------------------------------- depthwise / SE
-def dwconv_fwd(x, wdw, k, s, pad_t, pad_l, y):
+def dwconv_fwd(x, wdw, k, s, pad_t, pad_l, y, bn=None, act="none"):
+    """bn = (mean, invstd, gamma, beta): x is the producer's pre-BN tensor and the training-mode
+    BN + act is applied as the pixels are read (no materialised activation)."""
     n, h, w, c = x.shape
     _, oh, ow, _ = y.shape
-    lib().pld_dwconv_fwd(ptr(x), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow, ptr(y),
-                         stream())
+    if bn is None:
+        lib().pld_dwconv_fwd(ptr(x), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow, ptr(y),
+                             stream())
+    else:
+        mean, invstd, gamma, beta = bn
+        lib().pld_dwconv_fwd_bn(ptr(x), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow,
+                                ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ACT[act], ptr(y),
+                                stream())
 
 
 def dwconv_dgrad(dy, wdw, k, s, pad_t, pad_l, dx, accumulate=False):
@@ -473,8 +477,9 @@ def sampler_candidates(R, strategy):
 
 def sampler_compact(mask, gt, valid_idx, nvalid, gt_minmax):
     B, H, W = mask.shape
+    ws = workspace(lib().pld_sampler_compact_workspace_size(B, H, W), "compact")
     lib().pld_sampler_compact(ptr(mask), B, H, W, ptr(gt), ptr(valid_idx), ptr(nvalid),
-                              ptr(gt_minmax), None, stream())
+                              ptr(gt_minmax), ptr(ws), stream())
 
 
 def sampler_draw(nvalid, n_cand, L, seed, step, image_offset, draws):

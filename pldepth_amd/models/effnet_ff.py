@@ -47,6 +47,9 @@ DECODER = [
     ("dec_conv4", 32, None),
 ]
 # Keras' EfficientNet ImageNet checkpoint (TF 2.3-2.8) stores these in its Normalization layer
+# encoder activations the decoder concatenates (pl_hourglass.py:66,75,84): materialised
+SKIP_TAPS = tuple(skip for _, _, skip in DECODER if skip)
+
 IMAGENET_MEAN = [0.485, 0.456, 0.406]
 IMAGENET_VARIANCE = [0.229, 0.224, 0.225]
 
@@ -327,17 +330,25 @@ class EffNetFF:
     def _block_fwd(self, blk, x, training, step, li):
         A, B, n = self.act, self.B, blk["name"]
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
+        pt, pl = blk["pad"]
         if blk["ex"] != 1:
             K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"], math=self.enc_math),
                          blk["expand"].w_nat, None, A[n + "expand_pre"])
-            blk["expand_bn"].stats_(A[n + "expand_pre"], B * h * w, training)
-            blk["expand_bn"].apply(A[n + "expand_pre"], B * h * w, "swish",
-                                   A[n + "expand_activation"], training)
-            e = A[n + "expand_activation"]
+            ebn = blk["expand_bn"]
+            ebn.stats_(A[n + "expand_pre"], B * h * w, training)
+            if training and n + "expand_activation" not in SKIP_TAPS:
+                # BN + swish fused into the depthwise conv's input read: the activation is
+                # never materialised (only the decoder's skip taps need it)
+                K.dwconv_fwd(A[n + "expand_pre"], self.frozen[blk["dw"]], blk["k"], blk["s"],
+                             pt, pl, A[n + "dw_pre"],
+                             bn=(ebn.mean, ebn.invstd, ebn.gamma, ebn.beta), act="swish")
+            else:
+                ebn.apply(A[n + "expand_pre"], B * h * w, "swish", A[n + "expand_activation"],
+                          training)
+                K.dwconv_fwd(A[n + "expand_activation"], self.frozen[blk["dw"]], blk["k"],
+                             blk["s"], pt, pl, A[n + "dw_pre"])
         else:
-            e = x
-        pt, pl = blk["pad"]
-        K.dwconv_fwd(e, self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl, A[n + "dw_pre"])
+            K.dwconv_fwd(x, self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl, A[n + "dw_pre"])
         rows = B * oh * ow
         bn = blk["bn"]
         bn.stats_(A[n + "dw_pre"], rows, training)
@@ -461,9 +472,7 @@ class EffNetFF:
         if blk["ex"] != 1:
             ge = G[n + "expand_activation"]
             # skip taps already hold the decoder's gradient: accumulate onto it
-            is_tap = n + "expand_activation" in ("block6a_expand_activation",
-                                                 "block4a_expand_activation",
-                                                 "block3a_expand_activation")
+            is_tap = n + "expand_activation" in SKIP_TAPS
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
             gpe = self._gpre_buf(A[n + "expand_pre"].shape)
             blk["expand_bn"].bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)

@@ -341,7 +341,8 @@ def test_residual_and_per_sample_scale(cuda):
 # ------------------------------------------------------------------------- depthwise / SE
 @pytest.mark.parametrize("n,h,w,c,k,s", [(2, 12, 12, 16, 3, 1), (2, 12, 10, 24, 3, 2),
                                          (1, 14, 14, 40, 5, 2), (2, 7, 7, 8, 5, 1),
-                                         (1, 13, 11, 4, 3, 2)])
+                                         (1, 13, 11, 4, 3, 2), (1, 9, 13, 12, 5, 1),
+                                         (2, 15, 17, 8, 5, 2), (1, 5, 6, 4, 3, 1)])
 def test_dwconv(cuda, n, h, w, c, k, s):
     torch.manual_seed(k * 10 + s)
     x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
@@ -363,6 +364,35 @@ def test_dwconv(cuda, n, h, w, c, k, s):
     torch.cuda.synchronize()
     assert rel_err(y, y_ref) < 1e-5
     assert rel_err(dx, x.grad) < 1e-5
+
+
+@pytest.mark.parametrize("k,s", [(3, 1), (5, 2), (5, 1), (3, 2)])
+def test_dwconv_fused_bn_swish(cuda, k, s):
+    """pld_dwconv_fwd_bn == dwconv(swish(bn(x))) with batch statistics; padding taps read 0
+    (TF pads the activated tensor, not the pre-activation one)."""
+    n, h, w, c = 2, 11, 14, 24
+    torch.manual_seed(40 + k + s)
+    x = torch.randn(n, h, w, c, dtype=torch.float64) * 2 + 0.5
+    wk = torch.randn(k, k, c, dtype=torch.float64)
+    gamma = torch.rand(c, dtype=torch.float64) + 0.5
+    beta = torch.randn(c, dtype=torch.float64) * 0.2
+    mean = x.mean(dim=(0, 1, 2))
+    invstd = 1.0 / torch.sqrt(x.var(dim=(0, 1, 2), unbiased=False) + 1e-3)
+    a = (x - mean) * invstd * gamma + beta
+    a = a * torch.sigmoid(a)
+    if s == 2:
+        pt, pb = OE.correct_pad(h, k)
+        pl, pr = OE.correct_pad(w, k)
+    else:
+        pt, pb, _ = OE.same_pad(h, k, 1)
+        pl, pr, _ = OE.same_pad(w, k, 1)
+    y_ref = OE.dwconv(a.permute(0, 3, 1, 2), wk, s, (pt, pb, pl, pr)).permute(0, 2, 3, 1)
+    oh, ow = y_ref.shape[1:3]
+    y = torch.empty(n, oh, ow, c, device=cuda)
+    bn = tuple(dev(t, cuda) for t in (mean, invstd, gamma, beta))
+    K.dwconv_fwd(dev(x, cuda), dev(wk, cuda), k, s, pt, pl, y, bn=bn, act="swish")
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
 
 
 @pytest.mark.parametrize("n,h,w,c,cse", [(2, 6, 6, 96, 4), (3, 14, 14, 1152, 48),
@@ -419,6 +449,29 @@ def test_sampler_bit_exact_vs_oracle(cuda, golden, ci, strategy):
     assert nv.cpu().tolist() == [int(mask.sum())] * 2
     for b in range(B):
         np.testing.assert_array_equal(out[b].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("h,w", [(448, 448), (37, 53), (1, 5), (130, 129)])
+def test_sampler_compact_matches_np_where(cuda, h, w):
+    """Valid-pixel lists == np.where(mask > 0) order (sampling.py:135), nvalid, whole-image gt
+    min/max; images cover the empty mask, the full mask and ragged multi-segment sizes."""
+    rng = np.random.default_rng(h * 1000 + w)
+    B = 4
+    mask = (rng.random((B, h, w)) < 0.9).astype(np.float32)
+    mask[1] = 0.0
+    mask[2] = 1.0
+    gt = rng.random((B, h, w)).astype(np.float32)
+    gm, gg = dev(torch.from_numpy(mask), cuda), dev(torch.from_numpy(gt), cuda)
+    vi = torch.full((B, h * w), -7, dtype=torch.int32, device=cuda)
+    nv = torch.empty(B, dtype=torch.int32, device=cuda)
+    mm = torch.empty(B, 2, device=cuda)
+    K.sampler_compact(gm, gg, vi, nv, mm)
+    torch.cuda.synchronize()
+    for b in range(B):
+        ref = np.flatnonzero(mask[b].reshape(-1) > 0)
+        assert int(nv[b]) == ref.size
+        np.testing.assert_array_equal(vi[b, :ref.size].cpu().numpy(), ref)
+        assert float(mm[b, 0]) == gt[b].min() and float(mm[b, 1]) == gt[b].max()
 
 
 def test_sampler_draws_uniform_and_in_range(cuda):
