@@ -69,10 +69,10 @@ __device__ __forceinline__ float4 prologue4(int act, float4 v, float4 s, float4 
 // column routing (dgrad of a concat) and accumulate-or-overwrite are applied.
 template <int TM, int TN>
 __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx16 (&acc)[TM][TN],
-                                          int m_w, int n_w, int lane) {
+                                          int m_w, int n_w, int lane, int zb = -1) {
   const int h = lane >> 5, l32 = lane & 31;
   if (p.zstride > 0) {
-    float* out1 = p.out1 + (long)blockIdx.z * p.zstride;
+    float* out1 = p.out1 + (long)(zb >= 0 ? zb : (int)blockIdx.z) * p.zstride;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll

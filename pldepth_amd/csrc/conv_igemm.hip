@@ -674,8 +674,13 @@ extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
 constexpr int X3_BK = 32;
+// bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
+static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
 
-static bool x3_fwd_geom(int C, int c1) { return C % 8 == 0 && c1 % 8 == 0; }
+// bf16x3 eligibility: channel counts (vector staging) and no fused input prologue
+static bool x3_fwd_geom(int C, int c1, bool prologue, int taps) {
+  return C % 8 == 0 && c1 % 8 == 0 && !prologue && taps <= 32;
+}
 
 // Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), then
 // [2 n3, 2 n3 + kNumTiles) the exact-fp32 schedules — the per-shape autotuner may keep fp32
@@ -693,9 +698,10 @@ static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t) {
   if (geom_ok) x3 = true;
   else t = -1;
 }
-static bool x3_wgrad_geom(int c1, int c2, int cout) {
-  return c1 % 4 == 0 && c2 % 4 == 0 && cout % 4 == 0;
+static bool x3_wgrad_geom(int c1, int c2, int cout, bool prologue) {
+  return c1 % 4 == 0 && c2 % 4 == 0 && cout % 4 == 0 && !prologue;
 }
+extern "C" int pld_filter_split(const float* w, int64_t rows, int K, void* out, void* stream);
 
 // the x3 analogue of choose_tile (same cost model; WGRAD takes power-of-two tiles only)
 static int x3_choose(long M, long N, long K, int requested, bool wgrad) {
@@ -767,11 +773,22 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
                         size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
   bool x3;
-  resolve_sched(math, x3_fwd_geom(p.C, p.c1), tile, x3, tile);
+  resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
+                tile);
   if (x3) {
     PLD_CHECK_ARG(aligned16(p.x1) && (!p.x2 || aligned16(p.x2)) && aligned16(p.bmat) &&
                       (!p.bsplit || aligned16(p.bsplit)),
                   "%s: bf16x3 operands must be 16-byte aligned", who);
+    if (!p.bsplit) {  // the kernel stages a pre-split filter: split into the workspace's tail
+      const size_t sb = x3_split_bytes(p.N, p.K);
+      PLD_CHECK_ARG(ws && ws_bytes >= sb, "%s: workspace %zu < %zu bytes (filter split)", who,
+                    ws_bytes, sb);
+      ws_bytes -= sb;
+      float* wsp = (float*)((char*)ws + ws_bytes);
+      int rc = pld_filter_split(p.bmat, p.N, p.K, wsp, st);
+      if (rc) return rc;
+      p.bsplit = wsp;
+    }
     x3_fwd_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
     int bm, bn, tm, tn, occ;
     pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
@@ -816,13 +833,16 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   return check_launch("splitk_out_kernel");
 }
 
-static size_t fwd_ws_bytes(long M, long N, long K, int tile, int math = 0, bool geom = false) {
+static size_t fwd_ws_bytes(long M, long N, long K, int tile, int math = 0, bool geom = false,
+                           bool have_split = true) {
   int cfg, splits, kt_per;
   bool x3;
   resolve_sched(math, geom, tile, x3, tile);
   if (x3) x3_fwd_plan(M, N, K, tile, cfg, splits, kt_per);
   else fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
-  return splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  size_t b = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  if (x3 && !have_split) b = (b + 255) / 256 * 256 + x3_split_bytes(N, K);
+  return b;
 }
 
 extern "C" int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout,
@@ -882,7 +902,8 @@ extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (pld__skinny_eligible(a)) return 0;
   return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
                       (long)a->kh * a->kw * (a->c1 + a->c2), a->tile, a->math,
-                      x3_fwd_geom(a->c1 + a->c2, a->c1));
+                      x3_fwd_geom(a->c1 + a->c2, a->c1, a->in_scale != nullptr, a->kh * a->kw),
+                      a->w_split != nullptr);
 }
 
 static size_t strided_tmp_bytes(const pld_conv_args* a) {
@@ -892,12 +913,13 @@ static size_t strided_tmp_bytes(const pld_conv_args* a) {
 extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->h <= 0 || a->w <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;
-  const bool geom = x3_fwd_geom(a->cout, a->cout);
+  const bool geom = x3_fwd_geom(a->cout, a->cout, false, a->kh * a->kw);
+  const bool hs = a->w_split != nullptr;
   if (a->sh != 1 || a->sw != 1)  // 1x1 strided: GEMM into a compact tmp, then scatter
     return strided_tmp_bytes(a) + fwd_ws_bytes((long)a->n * a->oh * a->ow, a->c1 + a->c2,
-                                               a->cout, a->tile, a->math, geom);
+                                               a->cout, a->tile, a->math, geom, hs);
   return fwd_ws_bytes((long)a->n * a->h * a->w, a->c1 + a->c2, (long)a->kh * a->kw * a->cout,
-                      a->tile, a->math, geom);
+                      a->tile, a->math, geom, hs);
 }
 
 extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
@@ -1004,7 +1026,8 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
   N = a->cout;
   K = (long)a->n * a->oh * a->ow;
   int tile;
-  resolve_sched(a->math, x3_wgrad_geom(a->c1, a->c2, a->cout), a->tile, x3, tile);
+  resolve_sched(a->math, x3_wgrad_geom(a->c1, a->c2, a->cout, a->in_scale != nullptr), a->tile,
+                x3, tile);
   const int bk = x3 ? X3_BK : BK;
   const long ktiles = (K + bk - 1) / bk;
   // pick the tile for an unsplit GEMM, then split K until ~2-3 blocks per CU

@@ -16,15 +16,17 @@
 //
 // Tiling: 512 threads = 8 waves, warp-specialised. Waves 0-3 (consumers) own (BM/WM) x (BN/WN)
 // of the BM x BN block tile as 32x32 MFMA tiles; waves 4-7 (producers) stage the next 32-deep
-// K-step (global loads two steps ahead, fused prologue, hi/lo split, LDS stores), so the VALU
-// split work of one wave overlaps the matrix work of its SIMD partner. LDS holds, per operand
-// and buffer, a hi plane and a lo plane of [rows][4 x 16-byte k-chunks], XOR-swizzled (chunk_off) so that
-// the ds_read_b128 fragment reads (lane = row, 16 B = 8 k) and the row-per-lane stores are
-// conflict-free. Double-buffered, one barrier per K-step.
-//   FWD staging: wave w owns k-chunk w (8 consecutive k = 8 channels of one tap and one source,
-//     since C % 8 == 0), lane = row: the tap decomposition, the concat source and the fused
-//     input prologue's scale/shift are wave-uniform (scalar registers, one descriptor). A filter
-//     pre-split by pld_filter_split is staged as-is (no conversion).
+// K-step (global loads two steps ahead, hi/lo split, LDS stores), so the VALU split work of one
+// wave overlaps the matrix work of its SIMD partner. LDS holds, per operand and buffer, a hi
+// plane and a lo plane of [rows][4 x 16-byte k-chunks], XOR-swizzled (chunk_off) so that the
+// ds_read_b128 fragment reads (lane = row, 16 B = 8 k) and the producers' stores are
+// conflict-free. Double-buffered, one barrier per K-step. Workgroups are mapped to tiles
+// XCD-aware (neighbouring tiles share an XCD's L2).
+//   FWD/DGRAD staging: full 128-byte lines — 8 lanes per row, 4 consecutive k (channels of one
+//     tap and one source, since C % 8 == 0) per lane; the filter operand is pre-split
+//     (pld_filter_split; the host splits into the workspace when the caller has no copy) and
+//     staged as-is. The fused input prologue is not supported here (those convs take the fp32
+//     kernel).
 //   WGRAD staging: a thread owns 4 consecutive rows (channels) x P consecutive pixels and
 //     transposes them in registers into P-wide k runs of the 4 rows.
 #include <algorithm>
@@ -65,31 +67,6 @@ __device__ __forceinline__ bf16x8 lds_frag(const unsigned char* plane, int r, in
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + chunk_off(r, c)));
 }
 
-// act(x*s+t) on N values, the activation switch hoisted out of the element loop
-template <int N>
-__device__ __forceinline__ void prologue_n(int act, float (&e)[N], const float* s, const float* t) {
-  switch (act) {
-    case ACT_RELU:
-#pragma unroll
-      for (int u = 0; u < N; ++u) e[u] = fmaxf(e[u] * s[u] + t[u], 0.f);
-      break;
-    case ACT_SWISH:
-#pragma unroll
-      for (int u = 0; u < N; ++u) {
-        const float z = e[u] * s[u] + t[u];
-        e[u] = z * sigmoidf_(z);
-      }
-      break;
-    case ACT_SIGMOID:
-#pragma unroll
-      for (int u = 0; u < N; ++u) e[u] = sigmoidf_(e[u] * s[u] + t[u]);
-      break;
-    default:
-#pragma unroll
-      for (int u = 0; u < N; ++u) e[u] = e[u] * s[u] + t[u];
-  }
-}
-
 // LDS hand-off between the producer and consumer waves: the writer's ds_writes are complete
 // (lgkmcnt) before the barrier; no vmcnt wait, so the producers' next global loads stay in
 // flight across it. The empty asm statements keep the compiler from moving LDS accesses across.
@@ -111,14 +88,18 @@ struct X3Smem {
 };
 
 // ---------------------------------------------------------------------------- producer
-// Four waves (pw = 0..3) stage K-steps: global fp32 -> (prologue) -> bf16 hi/lo -> LDS.
-template <int BM, int BN, int MODE>
+// Four waves (pw = 0..3) stage K-steps: global fp32 -> bf16 hi/lo -> LDS. Every K-step issues
+// the same, unconditional set of loads (the concat's second source is a template parameter, the
+// last steps re-fetch the final tile), so the compiler can count the loads in flight and wait
+// for exactly one stage (vmcnt(N)), never draining the prefetch (vmcnt(0)).
+template <int BM, int BN, int MODE, bool CAT>
 __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned char* smem,
-                                            int kt_begin, int kt_end, int pw, int lane) {
+                                            int kt_begin, int kt_end, int pw, int lane, int mb,
+                                            int nb) {
   using S = X3Smem<BM, BN>;
   const int ptid = pw * 64 + lane;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const int m0 = mb * BM;
+  const int n0 = nb * BN;
 
   // x1/x2 addressed relative to the first image this workgroup touches (32-bit offsets)
   int img_base, pix_base = 0;
@@ -132,18 +113,28 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   const __amdgpu_buffer_rsrc_t rs1 =
       make_rsrc(p.x1 + img_base * img_elems * p.c1, (p.n - img_base) * img_elems * p.c1 * 4);
   const __amdgpu_buffer_rsrc_t rs2 =
-      p.c2 ? make_rsrc(p.x2 + img_base * img_elems * p.c2, (p.n - img_base) * img_elems * p.c2 * 4)
-           : make_rsrc(p.x1, 0);
-  const bool bsplit = MODE == MODE_FWD && p.bsplit != nullptr;  // B already hi/lo split
+      CAT ? make_rsrc(p.x2 + img_base * img_elems * p.c2, (p.n - img_base) * img_elems * p.c2 * 4)
+          : rs1;
+  // FWD: B is the pre-split filter (pld_filter_split layout); WGRAD: B = dY fp32
   const __amdgpu_buffer_rsrc_t rsb =
       (MODE == MODE_FWD)
-          ? make_rsrc(bsplit ? p.bsplit : p.bmat, (long)p.N * p.K * 4)
+          ? make_rsrc(p.bsplit, (long)p.N * p.K * 4)
           : make_rsrc(p.bmat + (long)pix_base * p.N, (long)(p.K - pix_base) * p.N * 4);
 
-  // FWD: lane = row (rows lane + 64 j), wave pw = k-chunk pw of the K-step
-  constexpr int FA = (BM + 63) / 64, FB = (BN + 63) / 64;
-  int a_ir[FA], a_iy0[FA], a_ix0[FA];
-  bool a_ok[FA];
+  // FWD: full-line staging. A wave-instruction covers 8 rows x 128 B: lane = (row lr = lane/8,
+  // 4-k group ks = lane%8); producer wave pw owns rows [pw BM/4, (pw+1) BM/4) of A and
+  // [pw BN/4, ...) of B, in groups of 8. B lanes 0-31 stage the hi halves, 32-63 the lo halves
+  // of 8 rows x 4 chunks (chunk = 32 B: [8 hi][8 lo] bf16).
+  static_assert(MODE != MODE_FWD || (BM % 32 == 0 && BN % 32 == 0), "FWD tiles: rows % 32");
+  constexpr int FA = BM / 32, FB = BN / 32;
+  const int lr = lane >> 3, ks = lane & 7;
+  const int br = lane & 31, half = lane >> 5;
+  // per A row: pixel index of tap (0,0) relative to the descriptor base, and the taps that land
+  // inside the image (bit t, taps <= 32); per B row: byte offset and validity
+  int a_base[FA];
+  unsigned a_taps[FA];
+  unsigned b_off[FB];
+  bool b_ok[FB];
   // WGRAD: thread = 4 rows (quad) x P consecutive pixels
   constexpr int QA = BM / 4, QB = BN / 4;
   constexpr int GA = 256 / QA, GB = 256 / QB;
@@ -151,23 +142,33 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   static_assert(MODE == MODE_FWD || (GA * PA == BK && GB * PB == BK && PA >= 1 && PB >= 1),
                 "WGRAD tile rows must be 32..256");
   int w_ty = 0, w_tx = 0, w_ci = 0;
-  bool w_ok = false, w_in1 = true, wpro = false;
-  float wsc[4] = {0.f, 0.f, 0.f, 0.f}, wsh[4] = {0.f, 0.f, 0.f, 0.f};
+  bool w_ok = false, w_in1 = true;
 
   if (MODE == MODE_FWD) {
 #pragma unroll
     for (int j = 0; j < FA; ++j) {
-      const int r = lane + 64 * j;
+      const int r = pw * (BM / 4) + 8 * j + lr;
       const int m = m0 + r;
-      a_ok[j] = (r < BM) && (m < p.M);
-      const int mm = a_ok[j] ? m : m0;
+      const bool mok = m < p.M;
+      const int mm = mok ? m : m0;
       const uint32_t q = p.dOW.div((uint32_t)mm);
       const int ox = mm - (int)q * p.ow;
       const uint32_t img = p.dOH.div(q);
       const int oy = (int)q - (int)img * p.oh;
-      a_ir[j] = ((int)img - img_base) * p.h;
-      a_iy0[j] = oy * p.sh - p.pt;
-      a_ix0[j] = ox * p.sw - p.pl;
+      const int iy0 = oy * p.sh - p.pt, ix0 = ox * p.sw - p.pl;
+      a_base[j] = (((int)img - img_base) * p.h + iy0) * p.w + ix0;
+      unsigned t = 0;
+      for (int ty = 0; ty < p.kh; ++ty)
+        for (int tx = 0; tx < p.kw; ++tx)
+          t |= (unsigned)(mok && (unsigned)(iy0 + ty) < (unsigned)p.h &&
+                          (unsigned)(ix0 + tx) < (unsigned)p.w) << (ty * p.kw + tx);
+      a_taps[j] = t;
+    }
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      const int nn = n0 + pw * (BN / 4) + 8 * j + (br >> 2);
+      b_ok[j] = nn < p.N;
+      b_off[j] = (unsigned)(b_ok[j] ? nn : 0) * (unsigned)p.K * 4u + 16u * half;
     }
   } else {
     const int i = m0 + 4 * (ptid % QA);
@@ -179,64 +180,41 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
     w_ty = (int)ty;
     w_tx = (int)tap - (int)ty * p.kw;
     w_in1 = w_ci < p.c1;
-    wpro = p.in_scale && w_ok && w_in1;
-    if (wpro) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        wsc[u] = p.in_scale[w_ci + u];
-        wsh[u] = p.in_shift[w_ci + u];
-      }
-    }
   }
 
-  constexpr int RA = (MODE == MODE_FWD) ? 2 * FA : PA;  // float4 staging registers, A
-  constexpr int RB = (MODE == MODE_FWD) ? 2 * FB : PB;  // and B
-  // one K-step in flight: its staging registers and per-step flags
-  struct Stage {
+  constexpr int RA = (MODE == MODE_FWD) ? FA : PA;  // float4 staging registers, A
+  constexpr int RB = (MODE == MODE_FWD) ? FB : PB;  // and B
+  struct Stage {  // one K-step in flight
     float4 ra[RA], rb[RB];
-    unsigned vmask;
-    bool fpro;  // FWD: the prologue applies to this K-step's chunk (wave-uniform)
-    int fci;    // FWD: first channel of the chunk (prologue coefficients)
   };
 
   auto load_tile = [&](int kt, Stage& st) {
-    float4* ra = st.ra;
-    float4* rb = st.rb;
-    unsigned& vmask = st.vmask;
     const int k0 = kt * BK;
-    vmask = 0;
     if (MODE == MODE_FWD) {
-      const int k = k0 + 8 * pw;  // wave-uniform
+      const int k = k0 + 4 * ks;  // this lane's 4 consecutive k (C % 8 == 0: one tap, one source)
       const bool kin = k < p.K;
       const int kk = kin ? k : 0;
       const int tap = (int)p.dC.div((uint32_t)kk);
       const int ci = kk - tap * p.C;
       const int ty = (int)p.dKW.div((uint32_t)tap);
-      const int tx = tap - ty * p.kw;
-      const bool src2 = ci >= p.c1;
+      const int toff = ty * p.w + (tap - ty * p.kw);  // pixel offset of the tap
+      const bool src2 = CAT && ci >= p.c1;
       const int cs = src2 ? p.c2 : p.c1;
       const int cb = src2 ? ci - p.c1 : ci;
-      const __amdgpu_buffer_rsrc_t rs = src2 ? rs2 : rs1;
 #pragma unroll
       for (int j = 0; j < FA; ++j) {
-        const int iy = a_iy0[j] + ty, ix = a_ix0[j] + tx;
-        const bool ok = kin && a_ok[j] && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-        const unsigned off = ok ? (unsigned)((((a_ir[j] + iy) * p.w + ix) * cs + cb) * 4) : OOB;
-        ra[2 * j] = bload4(rs, off);
-        ra[2 * j + 1] = bload4(rs, ok ? off + 16 : OOB);
-        vmask |= (unsigned)ok << j;
+        const bool ok = kin && ((a_taps[j] >> tap) & 1u);
+        const unsigned off = (unsigned)(((a_base[j] + toff) * cs + cb) * 4);
+        if (CAT)  // both sources, the other one out of range (reads as 0)
+          st.ra[j] = add4(bload4(rs1, (ok && !src2) ? off : OOB), bload4(rs2, (ok && src2) ? off : OOB));
+        else
+          st.ra[j] = bload4(rs1, ok ? off : OOB);
       }
-      st.fpro = p.in_scale && kin && !src2;
-      st.fci = ci;
+      const int kc = k0 + 8 * (br & 3);
+      const bool kcin = kc < p.K;
 #pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        const int r = lane + 64 * j;
-        const int n = n0 + r;
-        const bool ok = kin && r < BN && n < p.N;
-        const unsigned off = ok ? (unsigned)((n * p.K + k) * 4) : OOB;
-        rb[2 * j] = bload4(rsb, off);
-        rb[2 * j + 1] = bload4(rsb, ok ? off + 16 : OOB);
-      }
+      for (int j = 0; j < FB; ++j)
+        st.rb[j] = bload4(rsb, (b_ok[j] && kcin) ? b_off[j] + 4u * (unsigned)kc : OOB);
     } else {
       const int ga = ptid / QA;
 #pragma unroll
@@ -252,11 +230,11 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
         const int iy = oy * p.sh - p.pt + w_ty, ix = ox * p.sw - p.pl + w_tx;
         const bool ok = rok && w_ok && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
         const int px = (ir + iy) * p.w + ix;
-        float4 v = bload4(rs1, (ok && w_in1) ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB);
-        if (p.c2)
-          v = add4(v, bload4(rs2, (ok && !w_in1) ? (unsigned)((px * p.c2 + w_ci - p.c1) * 4) : OOB));
-        ra[j] = v;
-        vmask |= (unsigned)ok << j;
+        if (CAT)
+          st.ra[j] = add4(bload4(rs1, (ok && w_in1) ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB),
+                          bload4(rs2, (ok && !w_in1) ? (unsigned)((px * p.c2 + w_ci - p.c1) * 4) : OOB));
+        else
+          st.ra[j] = bload4(rs1, ok ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB);
       }
       const int gb = ptid / QB;
       const int n = n0 + 4 * (ptid % QB);
@@ -264,7 +242,7 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       for (int j = 0; j < PB; ++j) {
         const int pix = k0 + PB * gb + j;
         const bool ok = pix < p.K && n < p.N;
-        rb[j] = bload4(rsb, ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB);
+        st.rb[j] = bload4(rsb, ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB);
       }
     }
   };
@@ -301,63 +279,31 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   };
 
   auto store_tile = [&](int buf, const Stage& st) {
-    const float4* ra = st.ra;
-    const float4* rb = st.rb;
-    const unsigned vmask = st.vmask;
-    const bool fpro = st.fpro;
-    const int fci = st.fci;
     unsigned char* A = S::a(smem, buf);
     unsigned char* B = S::b(smem, buf);
     if (MODE == MODE_FWD) {
-      float sc[8], sh[8];
-      if (fpro) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          sc[u] = p.in_scale[fci + u];
-          sh[u] = p.in_shift[fci + u];
-        }
-      }
+      const int ob = 8 * (ks & 1);  // byte offset of this lane's 4 k inside its 16-byte chunk
 #pragma unroll
       for (int j = 0; j < FA; ++j) {
-        const int r = lane + 64 * j;
-        if (r >= BM) continue;
-        float e[8] = {ra[2 * j].x, ra[2 * j].y, ra[2 * j].z, ra[2 * j].w,
-                      ra[2 * j + 1].x, ra[2 * j + 1].y, ra[2 * j + 1].z, ra[2 * j + 1].w};
-        if (fpro && ((vmask >> j) & 1u)) prologue_n<8>(p.in_act, e, sc, sh);
-        unsigned hs[4], ls[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) split2(e[2 * u], e[2 * u + 1], hs[u], ls[u]);
-        const int o = chunk_off(r, pw);
-        *reinterpret_cast<u32x4*>(A + o) = u32x4{hs[0], hs[1], hs[2], hs[3]};
-        *reinterpret_cast<u32x4*>(A + S::A_PLANE + o) = u32x4{ls[0], ls[1], ls[2], ls[3]};
+        const int r = pw * (BM / 4) + 8 * j + lr;
+        unsigned h0, l0, h1, l1;
+        split2(st.ra[j].x, st.ra[j].y, h0, l0);
+        split2(st.ra[j].z, st.ra[j].w, h1, l1);
+        const int o = chunk_off(r, ks >> 1) + ob;
+        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(A + S::A_PLANE + o) = u32x2{l0, l1};
       }
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
-        const int r = lane + 64 * j;
-        if (r >= BN) continue;
-        const int o = chunk_off(r, pw);
-        if (bsplit) {  // chunk = [8 hi][8 lo] bf16, as written by pld_filter_split
-          *reinterpret_cast<float4*>(B + o) = rb[2 * j];
-          *reinterpret_cast<float4*>(B + S::B_PLANE + o) = rb[2 * j + 1];
-        } else {
-          const float e[8] = {rb[2 * j].x, rb[2 * j].y, rb[2 * j].z, rb[2 * j].w,
-                              rb[2 * j + 1].x, rb[2 * j + 1].y, rb[2 * j + 1].z, rb[2 * j + 1].w};
-          unsigned hs[4], ls[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) split2(e[2 * u], e[2 * u + 1], hs[u], ls[u]);
-          *reinterpret_cast<u32x4*>(B + o) = u32x4{hs[0], hs[1], hs[2], hs[3]};
-          *reinterpret_cast<u32x4*>(B + S::B_PLANE + o) = u32x4{ls[0], ls[1], ls[2], ls[3]};
-        }
+        const int r = pw * (BN / 4) + 8 * j + (br >> 2);
+        *reinterpret_cast<float4*>(B + half * S::B_PLANE + chunk_off(r, br & 3)) = st.rb[j];
       }
     } else {
       {
         float e[4][PA];
 #pragma unroll
         for (int j = 0; j < PA; ++j) {
-          float v[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
-          if (wpro && ((vmask >> j) & 1u)) prologue_n<4>(p.in_act, v, wsc, wsh);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) e[u][j] = v[u];
+          e[0][j] = st.ra[j].x; e[1][j] = st.ra[j].y; e[2][j] = st.ra[j].z; e[3][j] = st.ra[j].w;
         }
         store_quad(A, S::A_PLANE, ptid % QA, ptid / QA, e);
       }
@@ -365,45 +311,45 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
         float e[4][PB];
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
-          e[0][j] = rb[j].x; e[1][j] = rb[j].y; e[2][j] = rb[j].z; e[3][j] = rb[j].w;
+          e[0][j] = st.rb[j].x; e[1][j] = st.rb[j].y; e[2][j] = st.rb[j].z; e[3][j] = st.rb[j].w;
         }
         store_quad(B, S::B_PLANE, ptid % QB, ptid / QB, e);
       }
     }
   };
 
-  // Two register stages: K-step i+1 is stored while i runs on the MFMAs, and its registers
-  // are refilled with step i+3 — every global load has two K-steps of MFMA work to land.
-  // Barrier schedule (matches the consumer): 1 + n barriers.
+  // Two register stages: K-step i+1 is stored while i runs on the MFMAs and its registers are
+  // refilled with step i+3 (clamped to the last step: a harmless re-fetch) — every global load
+  // has two K-steps of MFMA work to land. Barriers (match the consumer): 1 + n.
   const int n = kt_end - kt_begin;
-  Stage s0, s1;
-  if (n > 0) {
-    load_tile(kt_begin, s0);
-    store_tile(0, s0);
-  }
-  if (n > 1) load_tile(kt_begin + 1, s0);
-  if (n > 2) load_tile(kt_begin + 2, s1);
-  lds_barrier();
-  for (int i = 0; i < n; i += 2) {
-    if (i + 1 < n) {
-      store_tile(1, s0);  // step i+1 (odd) -> buffer 1
-      if (i + 3 < n) load_tile(kt_begin + i + 3, s0);
-    }
+  if (n <= 0) {
     lds_barrier();
-    if (i + 1 < n) {
-      if (i + 2 < n) {
-        store_tile(0, s1);  // step i+2 (even) -> buffer 0
-        if (i + 4 < n) load_tile(kt_begin + i + 4, s1);
-      }
-      lds_barrier();
-    }
+    return;
+  }
+  const int last = kt_end - 1;
+  Stage s0, s1;
+  load_tile(kt_begin, s0);
+  store_tile(0, s0);
+  load_tile(min(kt_begin + 1, last), s0);
+  load_tile(min(kt_begin + 2, last), s1);
+  lds_barrier();
+  for (int i = 0;; i += 2) {
+    store_tile(1, s0);  // step i+1 (odd) -> buffer 1 (unused past the end)
+    load_tile(min(kt_begin + i + 3, last), s0);
+    lds_barrier();
+    if (i + 1 >= n) break;
+    store_tile(0, s1);  // step i+2 (even) -> buffer 0
+    load_tile(min(kt_begin + i + 4, last), s1);
+    lds_barrier();
+    if (i + 2 >= n) break;
   }
 }
 
 // ---------------------------------------------------------------------------- consumer
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned char* smem,
-                                            int kt_begin, int kt_end, int wave, int lane) {
+                                            int kt_begin, int kt_end, int wave, int lane, int mb,
+                                            int nb, int zb) {
   using S = X3Smem<BM, BN>;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -448,31 +394,47 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
     }
     lds_barrier();
   }
-  store_acc<TM, TN>(p, acc, blockIdx.x * BM + wm * WTM, blockIdx.y * BN + wn * WTN, lane);
+  store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane, zb);
 }
 
 // 512 threads: waves 0-3 consume (LDS fragments -> MFMA), waves 4-7 produce the next K-step
 // (global loads, prologue, hi/lo split, LDS stores) — a VALU-heavy wave and an MFMA-heavy
 // wave share each SIMD, so the split overlaps the matrix work.
-template <int BM, int BN, int WM, int WN, int MODE>
-__global__ __launch_bounds__(512) void conv_x3_kernel(GemmConvParams p) {
+template <int BM, int BN, int WM, int WN, int MODE, bool CAT>
+__global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvParams p) {
   static_assert(WM * WN == 4, "4 consumer waves");
   static_assert((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
   __shared__ __attribute__((aligned(16))) unsigned char smem[X3Smem<BM, BN>::BYTES];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (b, b+8, ... share
+  // one), so give each XCD a contiguous run of tiles, N fastest, then M, then the K split:
+  // the N tiles of one M tile (same A rows) and neighbouring M tiles (overlapping im2col
+  // halos) share that XCD's L2. Bijective for any grid size (speed only, never correctness).
+  const int nmb = gridDim.x, nnb = gridDim.y;
+  const int nwg = nmb * nnb * gridDim.z;
+  const int flat = blockIdx.x + nmb * (blockIdx.y + nnb * blockIdx.z);
+  const int xcd = flat & 7, slot = flat >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int nb = wid % nnb;
+  const int mb = (wid / nnb) % nmb;
+  const int zb = wid / (nnb * nmb);
   int kt_begin = 0, kt_end = (p.K + BK - 1) / BK;
   if (p.ktiles_per_split > 0) {
-    kt_begin = blockIdx.z * p.ktiles_per_split;
+    kt_begin = zb * p.ktiles_per_split;
     kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
   }
-  if (wave >= 4) x3_producer<BM, BN, MODE>(p, smem, kt_begin, kt_end, wave - 4, lane);
-  else x3_consumer<BM, BN, WM, WN>(p, smem, kt_begin, kt_end, wave, lane);
+  if (wave >= WM * WN)
+    x3_producer<BM, BN, MODE, CAT>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb, nb);
+  else
+    x3_consumer<BM, BN, WM, WN>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
 }
 
 // ------------------------------------------------------------------------ schedules
 struct Cfg { int bm, bn, tm, tn, occ; };
-// occ: resident 512-thread blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers)
+// occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
+// tiles per consumer wave.
 static const Cfg kCfg[] = {
     {256, 32, 2, 1, 2},  {128, 64, 2, 1, 3},  {128, 96, 1, 3, 2},  {128, 128, 2, 2, 2},
     {128, 160, 1, 5, 2}, {128, 192, 1, 6, 1}, {128, 224, 1, 7, 1}, {256, 64, 2, 2, 1},
@@ -487,7 +449,8 @@ template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(GemmConvParams& p, int splits, hipStream_t st) {
   if constexpr (MODE == MODE_FWD || (pow2_rows(BM) && pow2_rows(BN))) {
     dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
-    conv_x3_kernel<BM, BN, WM, WN, MODE><<<grid, 512, 0, st>>>(p);
+    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
+    else conv_x3_kernel<BM, BN, WM, WN, MODE, false><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
   }
 }
 
