@@ -699,7 +699,7 @@ static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t) {
   else t = -1;
 }
 static bool x3_wgrad_geom(int c1, int c2, int cout, bool prologue) {
-  return c1 % 4 == 0 && c2 % 4 == 0 && cout % 4 == 0 && !prologue;
+  return c1 % 16 == 0 && c2 % 16 == 0 && cout % 16 == 0 && !prologue;
 }
 extern "C" int pld_filter_split(const float* w, int64_t rows, int K, void* out, void* stream);
 

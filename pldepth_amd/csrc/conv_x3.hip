@@ -27,9 +27,11 @@
 //     (pld_filter_split; the host splits into the workspace when the caller has no copy) and
 //     staged as-is. The fused input prologue is not supported here (those convs take the fp32
 //     kernel).
-//   WGRAD staging: a thread owns 4 consecutive rows (channels) x P consecutive pixels and
-//     transposes them in registers into P-wide k runs of the 4 rows.
+//   WGRAD staging: lanes over 4-channel quads of one pixel (coalesced), stored row-contiguous
+//     into a [k = pixel][channel] image that the consumers read with ds_read_b64_tr_b16
+//     (hardware transpose) into the k-contiguous MFMA fragments.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "conv_common.h"
@@ -65,6 +67,35 @@ __device__ __forceinline__ int chunk_off(int r, int c) {
 
 __device__ __forceinline__ bf16x8 lds_frag(const unsigned char* plane, int r, int c) {
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + chunk_off(r, c)));
+}
+
+// WGRAD image: [32 k rows][R columns] bf16 per plane, 32-byte column blocks XOR-swizzled by
+// (k & 3) so a transposed read (4 rows x 16 columns per 16-lane group) touches distinct banks
+template <int R>
+__device__ __forceinline__ int tr_off(int k, int col) {
+  constexpr int NB = R / 16;  // 32-byte blocks per row
+  const int b = (col >> 4) ^ (((k & 3) << 1) & (NB - 1));
+  return k * (2 * R) + b * 32 + (col & 15) * 2;
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// 32x32x16 operand fragment from a [k][col] image with ds_read_b64_tr_b16: lane l needs
+// column c0 + (l & 31), k = 16 s + 8 (l >> 5) .. +7; each 16-lane group reads 4 k-rows x 16
+// columns per instruction (lane 4q+p supplies row q, columns 4p..4p+3) and receives its column
+template <int R>
+__device__ __forceinline__ bf16x8 lds_frag_tr(const unsigned char* plane, int c0, int s,
+                                              int lane) {
+  const int i16 = lane & 15, grp = (lane >> 4) & 1, h = lane >> 5;
+  const int k = 16 * s + 8 * h + (i16 >> 2);
+  const int col = c0 + 16 * grp + 4 * (i16 & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4s*)(plane + tr_off<R>(k, col)));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4s*)(plane + tr_off<R>(k + 4, col)));
+  const v4s v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // LDS hand-off between the producer and consumer waves: the writer's ds_writes are complete
@@ -135,12 +166,16 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   unsigned a_taps[FA];
   unsigned b_off[FB];
   bool b_ok[FB];
-  // WGRAD: thread = 4 rows (quad) x P consecutive pixels
-  constexpr int QA = BM / 4, QB = BN / 4;
-  constexpr int GA = 256 / QA, GB = 256 / QB;
-  constexpr int PA = BK / GA, PB = BK / GB;
-  static_assert(MODE == MODE_FWD || (GA * PA == BK && GB * PB == BK && PA >= 1 && PB >= 1),
-                "WGRAD tile rows must be 32..256");
+  // WGRAD: a thread owns 16 consecutive columns (fixed channels: one tap, one source, since
+  // C, c1 % 16 == 0) of P pixel slots g, g + G, ... of each K-step (NQ = R/16 threads per pixel
+  // row, G = 256/NQ rows per pass, P = max(1, 32/G); threads past row 31 idle). One pixel
+  // decomposition serves 16 channels; lanes run along a pixel row: 64-byte coalesced loads, and
+  // each thread fills one whole 32-byte block of the [k][col] image read back transposed.
+  constexpr int NQA = BM / 16, NQB = BN / 16;
+  constexpr int GA = 256 / NQA, GB = 256 / NQB;
+  constexpr int PA = GA >= BK ? 1 : BK / GA, PB = GB >= BK ? 1 : BK / GB;
+  static_assert(MODE == MODE_FWD || (BM >= 32 && BN >= 32 && BM <= 256 && BN <= 256),
+                "WGRAD tile columns must be 32..256");
   int w_ty = 0, w_tx = 0, w_ci = 0;
   bool w_ok = false, w_in1 = true;
 
@@ -171,7 +206,7 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       b_off[j] = (unsigned)(b_ok[j] ? nn : 0) * (unsigned)p.K * 4u + 16u * half;
     }
   } else {
-    const int i = m0 + 4 * (ptid % QA);
+    const int i = m0 + 16 * (ptid % NQA);
     w_ok = i < p.M;
     const int ii = w_ok ? i : 0;
     const uint32_t tap = p.dC.div((uint32_t)ii);
@@ -182,8 +217,8 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
     w_in1 = w_ci < p.c1;
   }
 
-  constexpr int RA = (MODE == MODE_FWD) ? FA : PA;  // float4 staging registers, A
-  constexpr int RB = (MODE == MODE_FWD) ? FB : PB;  // and B
+  constexpr int RA = (MODE == MODE_FWD) ? FA : 4 * PA;  // float4 staging registers, A
+  constexpr int RB = (MODE == MODE_FWD) ? FB : 4 * PB;  // and B
   struct Stage {  // one K-step in flight
     float4 ra[RA], rb[RB];
   };
@@ -216,11 +251,12 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       for (int j = 0; j < FB; ++j)
         st.rb[j] = bload4(rsb, (b_ok[j] && kcin) ? b_off[j] + 4u * (unsigned)kc : OOB);
     } else {
-      const int ga = ptid / QA;
+      const int ga = ptid / NQA;
 #pragma unroll
       for (int j = 0; j < PA; ++j) {
-        const int pix = k0 + PA * ga + j;
-        const bool rok = pix < p.K;
+        const int slot = ga + GA * j;
+        const int pix = k0 + slot;
+        const bool rok = slot < BK && pix < p.K;
         const int pp = rok ? pix : pix_base;
         const uint32_t q = p.dOW.div((uint32_t)pp);
         const int ox = pp - (int)q * p.ow;
@@ -230,52 +266,45 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
         const int iy = oy * p.sh - p.pt + w_ty, ix = ox * p.sw - p.pl + w_tx;
         const bool ok = rok && w_ok && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
         const int px = (ir + iy) * p.w + ix;
-        if (CAT)
-          st.ra[j] = add4(bload4(rs1, (ok && w_in1) ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB),
-                          bload4(rs2, (ok && !w_in1) ? (unsigned)((px * p.c2 + w_ci - p.c1) * 4) : OOB));
-        else
-          st.ra[j] = bload4(rs1, ok ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB);
+        const unsigned o1 = (ok && w_in1) ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB;
+        const unsigned o2 = (CAT && ok && !w_in1) ? (unsigned)((px * p.c2 + w_ci - p.c1) * 4) : OOB;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (CAT)
+            st.ra[4 * j + u] = add4(bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u),
+                                    bload4(rs2, o2 == OOB ? OOB : o2 + 16 * u));
+          else
+            st.ra[4 * j + u] = bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u);
+        }
       }
-      const int gb = ptid / QB;
-      const int n = n0 + 4 * (ptid % QB);
+      const int gb = ptid / NQB;
+      const int n = n0 + 16 * (ptid % NQB);
 #pragma unroll
       for (int j = 0; j < PB; ++j) {
-        const int pix = k0 + PB * gb + j;
-        const bool ok = pix < p.K && n < p.N;
-        st.rb[j] = bload4(rsb, ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB);
+        const int slot = gb + GB * j;
+        const int pix = k0 + slot;
+        const bool ok = slot < BK && pix < p.K && n < p.N;
+        const unsigned o = ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) st.rb[4 * j + u] = bload4(rsb, o == OOB ? OOB : o + 16 * u);
       }
     }
   };
 
-  // rows of 4-row quads x P k values -> P-wide runs in the hi and lo planes
-  auto store_quad = [&](unsigned char* plane, int plane_bytes, int q, int g, auto& e) {
-    constexpr int P = sizeof(e[0]) / sizeof(float);
+  // 16 columns of one k row -> one 32-byte block in each plane of the [k][col] image
+  auto store_row16 = [&](unsigned char* plane, int plane_bytes, auto rcols, int k, int col,
+                         const float4* v) {
+    unsigned h[8], l[8];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int r = 4 * q + u;
-      const int slot = P * g;
-      const int o = chunk_off(r, slot >> 3) + 2 * (slot & 7);
-      if constexpr (P == 1) {
-        const __bf16 hv = (__bf16)e[u][0];
-        const __bf16 lv = (__bf16)(e[u][0] - (float)hv);
-        *reinterpret_cast<__bf16*>(plane + o) = hv;
-        *reinterpret_cast<__bf16*>(plane + plane_bytes + o) = lv;
-      } else {
-        unsigned hi[P / 2], lo[P / 2];
-#pragma unroll
-        for (int t = 0; t < P / 2; ++t) split2(e[u][2 * t], e[u][2 * t + 1], hi[t], lo[t]);
-        if constexpr (P == 2) {
-          *reinterpret_cast<unsigned*>(plane + o) = hi[0];
-          *reinterpret_cast<unsigned*>(plane + plane_bytes + o) = lo[0];
-        } else if constexpr (P == 4) {
-          *reinterpret_cast<u32x2*>(plane + o) = u32x2{hi[0], hi[1]};
-          *reinterpret_cast<u32x2*>(plane + plane_bytes + o) = u32x2{lo[0], lo[1]};
-        } else {
-          *reinterpret_cast<u32x4*>(plane + o) = u32x4{hi[0], hi[1], hi[2], hi[3]};
-          *reinterpret_cast<u32x4*>(plane + plane_bytes + o) = u32x4{lo[0], lo[1], lo[2], lo[3]};
-        }
-      }
+      split2(v[u].x, v[u].y, h[2 * u], l[2 * u]);
+      split2(v[u].z, v[u].w, h[2 * u + 1], l[2 * u + 1]);
     }
+    const int o = tr_off<decltype(rcols)::value>(k, col);
+    *reinterpret_cast<u32x4*>(plane + o) = u32x4{h[0], h[1], h[2], h[3]};
+    *reinterpret_cast<u32x4*>(plane + o + 16) = u32x4{h[4], h[5], h[6], h[7]};
+    *reinterpret_cast<u32x4*>(plane + plane_bytes + o) = u32x4{l[0], l[1], l[2], l[3]};
+    *reinterpret_cast<u32x4*>(plane + plane_bytes + o + 16) = u32x4{l[4], l[5], l[6], l[7]};
   };
 
   auto store_tile = [&](int buf, const Stage& st) {
@@ -299,21 +328,19 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
         *reinterpret_cast<float4*>(B + half * S::B_PLANE + chunk_off(r, br & 3)) = st.rb[j];
       }
     } else {
-      {
-        float e[4][PA];
 #pragma unroll
-        for (int j = 0; j < PA; ++j) {
-          e[0][j] = st.ra[j].x; e[1][j] = st.ra[j].y; e[2][j] = st.ra[j].z; e[3][j] = st.ra[j].w;
-        }
-        store_quad(A, S::A_PLANE, ptid % QA, ptid / QA, e);
+      for (int j = 0; j < PA; ++j) {
+        const int slot = ptid / NQA + GA * j;
+        if (slot < BK)  // wave-uniform (idle waves of narrow tiles)
+          store_row16(A, S::A_PLANE, std::integral_constant<int, BM>{}, slot,
+                      16 * (ptid % NQA), &st.ra[4 * j]);
       }
-      {
-        float e[4][PB];
 #pragma unroll
-        for (int j = 0; j < PB; ++j) {
-          e[0][j] = st.rb[j].x; e[1][j] = st.rb[j].y; e[2][j] = st.rb[j].z; e[3][j] = st.rb[j].w;
-        }
-        store_quad(B, S::B_PLANE, ptid % QB, ptid / QB, e);
+      for (int j = 0; j < PB; ++j) {
+        const int slot = ptid / NQB + GB * j;
+        if (slot < BK)
+          store_row16(B, S::B_PLANE, std::integral_constant<int, BN>{}, slot,
+                      16 * (ptid % NQB), &st.rb[4 * j]);
       }
     }
   };
@@ -346,7 +373,7 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
 }
 
 // ---------------------------------------------------------------------------- consumer
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int MODE>
 __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned char* smem,
                                             int kt_begin, int kt_end, int wave, int lane, int mb,
                                             int nb, int zb) {
@@ -373,15 +400,25 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
       bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
-        const int r = wm * WTM + a * 32 + l32;
-        ah[a] = lds_frag(A, r, 2 * s + h);
-        al[a] = lds_frag(A + S::A_PLANE, r, 2 * s + h);
+        if constexpr (MODE == MODE_WGRAD) {
+          ah[a] = lds_frag_tr<BM>(A, wm * WTM + a * 32, s, lane);
+          al[a] = lds_frag_tr<BM>(A + S::A_PLANE, wm * WTM + a * 32, s, lane);
+        } else {
+          const int r = wm * WTM + a * 32 + l32;
+          ah[a] = lds_frag(A, r, 2 * s + h);
+          al[a] = lds_frag(A + S::A_PLANE, r, 2 * s + h);
+        }
       }
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int r = wn * WTN + b * 32 + l32;
-        bh[b] = lds_frag(B, r, 2 * s + h);
-        bl[b] = lds_frag(B + S::B_PLANE, r, 2 * s + h);
+        if constexpr (MODE == MODE_WGRAD) {
+          bh[b] = lds_frag_tr<BN>(B, wn * WTN + b * 32, s, lane);
+          bl[b] = lds_frag_tr<BN>(B + S::B_PLANE, wn * WTN + b * 32, s, lane);
+        } else {
+          const int r = wn * WTN + b * 32 + l32;
+          bh[b] = lds_frag(B, r, 2 * s + h);
+          bl[b] = lds_frag(B + S::B_PLANE, r, 2 * s + h);
+        }
       }
 #pragma unroll
       for (int a = 0; a < TM; ++a)
@@ -428,7 +465,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvPar
   if (wave >= WM * WN)
     x3_producer<BM, BN, MODE, CAT>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb, nb);
   else
-    x3_consumer<BM, BN, WM, WN>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
+    x3_consumer<BM, BN, WM, WN, MODE>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
 }
 
 // ------------------------------------------------------------------------ schedules
