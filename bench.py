@@ -21,6 +21,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (spec, no sparsity)
+# per conv kernel family (pld_conv_kernel_kind): peak in fp32-equivalent algorithmic TFLOP/s;
+# bf16x3 spends three bf16 MFMA products per fp32 product.
+KIND_PEAK = {0: FP32_MFMA_PEAK_TFLOPS, 1: BF16_MFMA_PEAK_TFLOPS / 3.0, 2: FP32_MFMA_PEAK_TFLOPS}
+KIND_NAME = {0: "fp32_mfma", 1: "bf16x3_mfma", 2: "direct_valu"}
 
 
 def synthetic_batch(B, H, W, seed):
@@ -43,14 +48,17 @@ def synthetic_batch(B, H, W, seed):
 
 
 def profile_conv(trainer, lr):
-    """One eager step with HIP events around every implicit-GEMM conv launch (on the stream the
-    kernels run on). Returns (algorithmic FLOPs, seconds) of the conv_igemm family."""
+    """One eager step with HIP events around every conv launch (on the stream the kernels run
+    on). Returns {kernel family (pld_conv_kernel_kind): [algorithmic FLOPs, seconds, launches]}."""
+    import ctypes
     from pldepth_amd import kernels as K
+    from pldepth_amd._lib import lib
     st = trainer.stream
     recs = []
     orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad")}
+    mode_of = {"conv2d_fwd": 0, "conv2d_dgrad": 1, "conv2d_wgrad": 2}
 
-    def flops_of(name, a):
+    def flops_of(a):
         # fwd, dX and dW of one conv are the same contraction: 2 * outputs * taps * Cin * Cout
         return 2.0 * a.n * a.oh * a.ow * a.cout * a.kh * a.kw * (a.c1 + a.c2)
 
@@ -62,7 +70,8 @@ def profile_conv(trainer, lr):
             e0.record(st)
             r = fn(args, *rest, **kw)
             e1.record(st)
-            recs.append((flops_of(name, args), e0, e1))
+            kind = lib().pld_conv_kernel_kind(ctypes.byref(args), mode_of[name])
+            recs.append((kind, flops_of(args), e0, e1))
             return r
         return w
 
@@ -74,9 +83,41 @@ def profile_conv(trainer, lr):
     finally:
         for n, f in orig.items():
             setattr(K, n, f)
-    fl = sum(r[0] for r in recs)
-    sec = sum(r[1].elapsed_time(r[2]) for r in recs) / 1e3
-    return fl, sec, len(recs)
+    out = {}
+    for kind, fl, e0, e1 in recs:
+        d = out.setdefault(kind, [0.0, 0.0, 0])
+        d[0] += fl
+        d[1] += e0.elapsed_time(e1) / 1e3
+        d[2] += 1
+    return out
+
+
+def conv_roofline(prof, traffic_file):
+    """roofline object of the conv family. achieved = algorithmic FLOPs / measured time; peak =
+    the FLOP-weighted harmonic mean of the families' peaks (the same FLOPs, each family at its
+    own peak); traffic = HBM bytes per launch from the committed PMC summary when present."""
+    fl = sum(v[0] for v in prof.values())
+    sec = sum(v[1] for v in prof.values())
+    n = sum(v[2] for v in prof.values())
+    t_peak = sum(v[0] / (KIND_PEAK[k] * 1e12) for k, v in prof.items())
+    achieved = fl / sec / 1e12
+    peak = fl / t_peak / 1e12
+    traffic = None
+    if traffic_file and os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            traffic = json.load(f).get("conv_bytes_per_launch")
+    return {
+        "bound": "mfma",
+        "kernel": "conv family: conv_x3_kernel (bf16x3 MFMA) + conv_igemm_kernel (fp32 MFMA) "
+                  "+ direct Cout=1 kernels; fwd/dgrad/wgrad",
+        "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
+        "flops_per_step": fl,
+        "families": {KIND_NAME[k]: {"tflop": round(v[0] / 1e12, 4), "ms": round(v[1] * 1e3, 3),
+                                    "launches": v[2], "achieved": round(v[0] / v[1] / 1e12, 2),
+                                    "peak": round(KIND_PEAK[k], 1)}
+                     for k, v in sorted(prof.items())},
+    }
 
 
 def cpu_baseline(H, W, L, R, model="ff_effnet", seconds_budget=25.0):
@@ -180,6 +221,8 @@ def main():
     ap.add_argument("--conv-math", default="mixed", choices=["mixed", "bf16x3", "fp32"],
                     help="conv arithmetic policy (kernels.conv_policy): mixed = encoder fp32, "
                          "decoder bf16x3")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "conv_traffic.json"),
+                    help="PMC traffic summary of the conv family (tools/traffic.py --json)")
     ap.add_argument("--tile-cache", default="",
                     help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
@@ -247,10 +290,11 @@ def main():
     loss = tr.loss_value()
     value = world * B * a.steps / elapsed
 
-    # conv_igemm family: algorithmic FLOPs / measured duration (HIP events, eager step)
-    fl, sec, nlaunch = profile_conv(tr, lr)
-    achieved = fl / sec / 1e12
+    # conv family: algorithmic FLOPs / measured duration (HIP events, eager step)
+    prof = profile_conv(tr, lr)
     flops_img = tr.engine.conv_flops_per_image()
+    roof = conv_roofline(prof, a.traffic_file)
+    roof["step_frac"] = round(value / world * flops_img / 1e12 / roof["peak"], 4)
     out = {
         "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
         "value": round(value, 3),
@@ -271,13 +315,9 @@ def main():
                    "model": a.model, "global_batch": world * B, "input": f"{H}x{W}",
                    "ranking_size": L, "rankings_per_image": R,
                    "parallelism": f"dp{world}", "graph": not a.no_graph},
-        "roofline": {
-            "bound": "mfma", "kernel": "conv_igemm_kernel (fwd/dgrad/wgrad, fp32 MFMA)",
-            "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "launches": nlaunch, "flops_per_step": fl,
-            "step_frac": round(value / world * flops_img / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-        },
+        "conv_math": {"policy": a.conv_math, "encoder": tr.engine.enc_math,
+                      "decoder": tr.engine.dec_math},
+        "roofline": roof,
         "loss": loss,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -124,6 +124,12 @@ enum { PLD_MATH_FP32 = 0, PLD_MATH_BF16X3 = 1 };
 int pld_conv_num_tiles(void);
 /* the same for a given PLD_MATH_* */
 int pld_conv_num_schedules(int math);
+/* which kernel family a conv call runs (mode 0 = fwd, 1 = dgrad, 2 = wgrad) for its math and
+ * tile: PLD_KIND_FP32 (v_mfma_f32_32x32x2_f32), PLD_KIND_BF16X3 (v_mfma_f32_32x32x16_bf16 x3) or
+ * PLD_KIND_DIRECT (single-output-channel VALU kernels); -1 on bad arguments. For roofline
+ * accounting (each family has its own peak). */
+enum { PLD_KIND_FP32 = 0, PLD_KIND_BF16X3 = 1, PLD_KIND_DIRECT = 2 };
+int pld_conv_kernel_kind(const pld_conv_args* a, int mode);
 size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a);
 size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a);
 

@@ -897,6 +897,22 @@ extern "C" int pld_conv_num_schedules(int math) {
   return math == PLD_MATH_BF16X3 ? 2 * pld__x3_num_cfg() + kNumTiles : kNumTiles;
 }
 
+extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
+  if (!a || mode < 0 || mode > 2) return -1;
+  if (pld__skinny_eligible(a) && !(mode == 1 && (a->sh != 1 || a->sw != 1)))
+    return PLD_KIND_DIRECT;
+  bool geom, x3;
+  int t;
+  if (mode == 2)
+    geom = x3_wgrad_geom(a->c1, a->c2, a->cout, a->in_scale != nullptr);
+  else if (mode == 1)
+    geom = x3_fwd_geom(a->cout, a->cout, false, a->kh * a->kw);
+  else
+    geom = x3_fwd_geom(a->c1 + a->c2, a->c1, a->in_scale != nullptr, a->kh * a->kw);
+  resolve_sched(a->math, geom, a->tile, x3, t);
+  return x3 ? PLD_KIND_BF16X3 : PLD_KIND_FP32;
+}
+
 extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;

@@ -9,7 +9,12 @@ profiling step; durations come from the same passes' kernel trace.
 import argparse
 import collections
 import csv
+import json
 import os
+
+CONV_MAIN = ("conv_igemm_kernel", "conv_x3_kernel", "skinny_fwd_kernel", "skinny_dgrad_kernel",
+             "skinny_wgrad_kernel")
+CONV_KERNELS = CONV_MAIN + ("splitk_", "stride_scatter_kernel", "skinny_wgrad_reduce_kernel")
 
 
 def load(d, counter):
@@ -34,6 +39,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--marker", default="adam_amsgrad_dev_kernel")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--json", default="", help="write the conv-family summary (bench.py "
+                                               "--traffic-file) here")
     a = ap.parse_args()
     f = window(load(os.path.join(a.dir, "fetch"), "FETCH_SIZE"), a.marker)
     w = window(load(os.path.join(a.dir, "write"), "WRITE_SIZE"), a.marker)
@@ -55,6 +62,22 @@ def main():
         bw = (g[1] + g[2]) / max(g[3], 1)
         print(f"{g[0]:5d} {g[3] / 1e6:7.3f} {g[1] / 1e9:8.3f} {g[2] / 1e9:8.3f} {bw:7.0f}  "
               f"{name[:90]}")
+    if a.json:
+        # the conv family as bench.py's roofline counts it: one conv call = its main kernel plus
+        # the split-K / stride reductions it launches
+        conv = {n: g for n, g in agg.items() if any(k in n for k in CONV_KERNELS)}
+        calls = sum(g[0] for n, g in conv.items() if any(k in n for k in CONV_MAIN))
+        rb = sum(g[1] for g in conv.values())
+        wb = sum(g[2] for g in conv.values())
+        out = {"source": a.dir, "step_read_bytes": tot_r, "step_write_bytes": tot_w,
+               "conv_read_bytes_per_step": rb, "conv_write_bytes_per_step": wb,
+               "conv_calls_per_step": calls,
+               "conv_bytes_per_launch": round((rb + wb) / max(calls, 1)),
+               "note": "FETCH_SIZE x2 (gfx950 64-B tally of 128-B reads) + WRITE_SIZE, separate "
+                       "--pmc passes, eager step window between adam_amsgrad_dev_kernel markers"}
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+        print(f"conv family: {(rb + wb) / 1e9:.2f} GB/step over {calls} calls -> {a.json}")
 
 
 if __name__ == "__main__":
