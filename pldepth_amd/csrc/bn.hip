@@ -73,7 +73,47 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
       ld<VW>(p.gamma + c0, gam);
       ld<VW>(p.beta + c0, bet);
     }
-    for (long r = rbeg + r0; r < rend; r += rpi) {
+    long r = rbeg + r0;
+    if (OP != RED_BNBWD) {
+      // RU independent row loads in flight per thread before any is consumed (one load per
+      // thread per trip leaves too few bytes in flight to cover HBM latency). Same summation
+      // order as the plain loop.
+      constexpr int RU = 4;
+      for (; r + (RU - 1) * rpi < rend; r += RU * rpi) {
+        float xv[RU][VW];
+#pragma unroll
+        for (int j = 0; j < RU; ++j) ld<VW>(p.x + (r + j * rpi) * p.C + c0, xv[j]);
+#pragma unroll
+        for (int j = 0; j < RU; ++j)
+#pragma unroll
+          for (int u = 0; u < VW; ++u) {
+            const double d = xv[j][u];
+            s0[u] += d;
+            if (OP == RED_STATS) s1[u] += d * d;
+          }
+      }
+    } else if (!p.gate && !p.addn && !p.res) {  // plain BN(+act) backward: same, for (x, dy)
+      constexpr int RU = 4;
+      for (; r + (RU - 1) * rpi < rend; r += RU * rpi) {
+        float xv[RU][VW], dv[RU][VW];
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+          ld<VW>(p.x + (r + j * rpi) * p.C + c0, xv[j]);
+          ld<VW>(p.dy + (r + j * rpi) * p.C + c0, dv[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < RU; ++j)
+#pragma unroll
+          for (int u = 0; u < VW; ++u) {
+            const float xh = (xv[j][u] - mean[u]) * inv[u];
+            const float z = xh * gam[u] + bet[u];
+            const float dz = dv[j][u] * act_grad(p.act, z);
+            s0[u] += (double)dz;
+            s1[u] += (double)dz * (double)xh;
+          }
+      }
+    }
+    for (; r < rend; r += rpi) {
       float xv[VW];
       ld<VW>(p.x + r * p.C + c0, xv);
       if (OP == RED_STATS) {

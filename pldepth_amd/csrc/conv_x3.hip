@@ -69,12 +69,20 @@ __device__ __forceinline__ bf16x8 lds_frag(const unsigned char* plane, int r, in
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + chunk_off(r, c)));
 }
 
-// WGRAD image: [32 k rows][R columns] bf16 per plane, 32-byte column blocks XOR-swizzled by
-// (k & 3) so a transposed read (4 rows x 16 columns per 16-lane group) touches distinct banks
+// WGRAD image: [32 k rows][R columns] bf16 per plane. A transposed read (4 consecutive k rows x
+// 32 bytes per 16-lane group, the second group 32 bytes further) must touch distinct banks:
+// with a row pitch that is a multiple of 256 B (R = 32, 64, 128, 256) the 32-byte column blocks
+// are XOR-swizzled by 2(k & 3); a pitch of 320, 192 or 448 B (R = 160, 96, 224) already puts the
+// four rows 16 banks apart; R = 192 (384 B: rows alternate between two bank offsets) swaps block
+// pairs on k & 2.
 template <int R>
 __device__ __forceinline__ int tr_off(int k, int col) {
   constexpr int NB = R / 16;  // 32-byte blocks per row
-  const int b = (col >> 4) ^ (((k & 3) << 1) & (NB - 1));
+  static_assert(R % 32 == 0 && R >= 32 && R <= 256, "WGRAD image width");
+  int sw = 0;
+  if constexpr ((NB & (NB - 1)) == 0) sw = ((k & 3) << 1) & (NB - 1);
+  else if constexpr (NB == 12) sw = k & 2;
+  const int b = (col >> 4) ^ sw;
   return k * (2 * R) + b * 32 + (col & 15) * 2;
 }
 
@@ -168,12 +176,13 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   bool b_ok[FB];
   // WGRAD: a thread owns 16 consecutive columns (fixed channels: one tap, one source, since
   // C, c1 % 16 == 0) of P pixel slots g, g + G, ... of each K-step (NQ = R/16 threads per pixel
-  // row, G = 256/NQ rows per pass, P = max(1, 32/G); threads past row 31 idle). One pixel
-  // decomposition serves 16 channels; lanes run along a pixel row: 64-byte coalesced loads, and
-  // each thread fills one whole 32-byte block of the [k][col] image read back transposed.
+  // row, G = floor(256/NQ) rows per pass, P = ceil(32/G); threads past row 31, and the
+  // 256 mod NQ threads past the last full pass, idle). One pixel decomposition serves 16
+  // channels; lanes run along a pixel row: 64-byte coalesced loads, and each thread fills one
+  // whole 32-byte block of the [k][col] image read back transposed.
   constexpr int NQA = BM / 16, NQB = BN / 16;
   constexpr int GA = 256 / NQA, GB = 256 / NQB;
-  constexpr int PA = GA >= BK ? 1 : BK / GA, PB = GB >= BK ? 1 : BK / GB;
+  constexpr int PA = (BK + GA - 1) / GA, PB = (BK + GB - 1) / GB;
   static_assert(MODE == MODE_FWD || (BM >= 32 && BN >= 32 && BM <= 256 && BN <= 256),
                 "WGRAD tile columns must be 32..256");
   int w_ty = 0, w_tx = 0, w_ci = 0;
@@ -256,7 +265,7 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       for (int j = 0; j < PA; ++j) {
         const int slot = ga + GA * j;
         const int pix = k0 + slot;
-        const bool rok = slot < BK && pix < p.K;
+        const bool rok = ga < GA && slot < BK && pix < p.K;
         const int pp = rok ? pix : pix_base;
         const uint32_t q = p.dOW.div((uint32_t)pp);
         const int ox = pp - (int)q * p.ow;
@@ -283,7 +292,7 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       for (int j = 0; j < PB; ++j) {
         const int slot = gb + GB * j;
         const int pix = k0 + slot;
-        const bool ok = slot < BK && pix < p.K && n < p.N;
+        const bool ok = gb < GB && slot < BK && pix < p.K && n < p.N;
         const unsigned o = ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB;
 #pragma unroll
         for (int u = 0; u < 4; ++u) st.rb[4 * j + u] = bload4(rsb, o == OOB ? OOB : o + 16 * u);
@@ -331,14 +340,14 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
 #pragma unroll
       for (int j = 0; j < PA; ++j) {
         const int slot = ptid / NQA + GA * j;
-        if (slot < BK)  // wave-uniform (idle waves of narrow tiles)
+        if (ptid / NQA < GA && slot < BK)
           store_row16(A, S::A_PLANE, std::integral_constant<int, BM>{}, slot,
                       16 * (ptid % NQA), &st.ra[4 * j]);
       }
 #pragma unroll
       for (int j = 0; j < PB; ++j) {
         const int slot = ptid / NQB + GB * j;
-        if (slot < BK)
+        if (ptid / NQB < GB && slot < BK)
           store_row16(B, S::B_PLANE, std::integral_constant<int, BN>{}, slot,
                       16 * (ptid % NQB), &st.rb[4 * j]);
       }
@@ -479,16 +488,11 @@ static const Cfg kCfg[] = {
 };
 constexpr int kNumCfg = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
 
-// WGRAD stages rows as 4-row quads x P pixels: BM and BN must be powers of two in [32, 256]
-constexpr bool pow2_rows(int r) { return r == 32 || r == 64 || r == 128 || r == 256; }
-
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(GemmConvParams& p, int splits, hipStream_t st) {
-  if constexpr (MODE == MODE_FWD || (pow2_rows(BM) && pow2_rows(BN))) {
-    dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
-    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
-    else conv_x3_kernel<BM, BN, WM, WN, MODE, false><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
-  }
+  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
+  if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
+  else conv_x3_kernel<BM, BN, WM, WN, MODE, false><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
 }
 
 template <int MODE>
@@ -545,9 +549,8 @@ extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int
   *bm = c.bm; *bn = c.bn; *tm = c.tm; *tn = c.tn; *occ = c.occ;
   return PLD_OK;
 }
-extern "C" int pld__x3_wgrad_cfg_ok(int cfg) {
-  return cfg >= 0 && cfg < x3::kNumCfg && x3::pow2_rows(x3::kCfg[cfg].bm) &&
-         x3::pow2_rows(x3::kCfg[cfg].bn);
+extern "C" int pld__x3_wgrad_cfg_ok(int cfg) {  // every tile (widths 32..256, % 32)
+  return cfg >= 0 && cfg < x3::kNumCfg;
 }
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {

@@ -178,7 +178,8 @@ def test_conv_fwd_dgrad_wgrad(cuda, case, math):
 @pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("case", [(2, 14, 14, 96, 32, 3, 1, 64, True),
                                   (1, 9, 11, 64, 0, 1, 1, 320, False),
-                                  (2, 10, 9, 48, 24, 3, 1, 136, True)])
+                                  (2, 10, 9, 48, 24, 3, 1, 136, True),
+                                  (2, 12, 10, 32, 16, 3, 1, 144, False)])
 def test_conv_every_schedule(cuda, case, math):
     """Each tile x split-K schedule computes the same conv (fwd with bias routing, dgrad into
     two concat destinations with accumulate)."""
