@@ -37,7 +37,11 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // ---- activations (Keras semantics) ----
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
 
-__device__ __forceinline__ float sigmoidf_(float z) { return 1.0f / (1.0f + __expf(-z)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp each): the IEEE division's scale/fixup sequence cost ~10
+// instructions per activation in the kernels that re-apply BN + activation on every read
+__device__ __forceinline__ float sigmoidf_(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+}
 
 __device__ __forceinline__ float act_fwd(int act, float z) {
   switch (act) {

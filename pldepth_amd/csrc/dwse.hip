@@ -12,7 +12,7 @@
 // fixed-order finalize); the two tiny FCs run one workgroup per image.
 #include <algorithm>
 
-#include "common.h"
+#include "conv_common.h"
 
 namespace pld {
 
@@ -36,23 +36,34 @@ __device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
   return acc;
 }
 
-// forward: a thread owns T consecutive output columns of one row and 4 channels; the K rows of
-// its (T-1)S+K input columns are loaded once each (register window), instead of K*K per output.
-template <int K, int S, int T, bool PRO>
+// forward: a thread owns an R x T block of output pixels (R rows, T consecutive columns) and 4
+// channels; each of the (R-1)S+K input rows of its (T-1)S+K-column window is loaded — and, with
+// the BN+activation prologue, activated — once, then feeds every output row it reaches (the
+// prologue's exp/rcp were the cost of a one-row window). Per output the taps are summed in the
+// same (ty, tx) order as a direct loop. The prologue activation ACT is a template parameter
+// (PRO_NONE: no prologue). The loads stay behind per-row/column bounds branches on purpose:
+// branch-free (buffer-descriptor) loads let hipcc hoist every row's loads ahead of the FMAs
+// (> 256 VGPRs, spills for K = 5).
+constexpr int PRO_NONE = -1;
+
+template <int K, int S, int T, int R, int ACT>
 __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ x,
                                                          const float* __restrict__ wt, DwGeom g,
                                                          float* __restrict__ y) {
+  constexpr bool PRO = ACT != PRO_NONE;
   constexpr int NC = (T - 1) * S + K;
+  constexpr int NR = (R - 1) * S + K;
   const int cv = g.c / 4;
   const int tiles = (g.ow + T - 1) / T;
-  const int total = g.n * g.oh * tiles * cv;
+  const int rgroups = (g.oh + R - 1) / R;
+  const int total = g.n * rgroups * tiles * cv;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int t0 = (int)g.dCV.div((uint32_t)e);
     const int q = e - t0 * cv;
     const int t1 = (int)g.dTiles.div((uint32_t)t0);
     const int ox0 = (t0 - t1 * tiles) * T;
     const int img = (int)g.dRows.div((uint32_t)t1);
-    const int oy = t1 - img * g.oh;
+    const int oy0 = (t1 - img * rgroups) * R;
     float4 mu, is, ga, be;
     if (PRO) {
       mu = *reinterpret_cast<const float4*>(g.mean + 4 * q);
@@ -60,71 +71,88 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
       ga = *reinterpret_cast<const float4*>(g.gamma + 4 * q);
       be = *reinterpret_cast<const float4*>(g.beta + 4 * q);
     }
-    float4 acc[T];
+    float4 acc[R][T];
 #pragma unroll
-    for (int o = 0; o < T; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int o = 0; o < T; ++o) acc[r][o] = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* xb = x + (long)img * g.h * g.w * g.c + 4 * q;
     const int ix0 = ox0 * S - g.pl;
 #pragma unroll
-    for (int ty = 0; ty < K; ++ty) {
-      const int iy = oy * S + ty - g.pt;
+    for (int j = 0; j < NR; ++j) {
+      const int iy = oy0 * S + j - g.pt;
       if (iy < 0 || iy >= g.h) continue;
       float4 row[NC];
 #pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const int ix = ix0 + j;
+      for (int jc = 0; jc < NC; ++jc) {
+        const int ix = ix0 + jc;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ix >= 0 && ix < g.w) {
           v = *reinterpret_cast<const float4*>(xb + ((long)iy * g.w + ix) * g.c);
-          if (PRO) {  // the bn_apply arithmetic, then the activation (TF pads the activated map)
-            v = make_float4(act_fwd(g.act, ((v.x - mu.x) * is.x) * ga.x + be.x),
-                            act_fwd(g.act, ((v.y - mu.y) * is.y) * ga.y + be.y),
-                            act_fwd(g.act, ((v.z - mu.z) * is.z) * ga.z + be.z),
-                            act_fwd(g.act, ((v.w - mu.w) * is.w) * ga.w + be.w));
-          }
+          if (PRO)  // the bn_apply arithmetic, then the activation (TF pads the activated map)
+            v = make_float4(act_fwd(ACT, ((v.x - mu.x) * is.x) * ga.x + be.x),
+                            act_fwd(ACT, ((v.y - mu.y) * is.y) * ga.y + be.y),
+                            act_fwd(ACT, ((v.z - mu.z) * is.z) * ga.z + be.z),
+                            act_fwd(ACT, ((v.w - mu.w) * is.w) * ga.w + be.w));
         }
-        row[j] = v;
+        row[jc] = v;
       }
+      const float* wq = wt + 4 * q;
 #pragma unroll
-      for (int tx = 0; tx < K; ++tx) {
-        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
+      for (int r = 0; r < R; ++r) {
+        const int ty = j - r * S;  // compile-time after unrolling
+        if (ty < 0 || ty >= K) continue;
 #pragma unroll
-        for (int o = 0; o < T; ++o) acc[o] = fma4(acc[o], row[o * S + tx], f);
+        for (int tx = 0; tx < K; ++tx) {
+          const float4 f = *reinterpret_cast<const float4*>(wq + (ty * K + tx) * g.c);
+#pragma unroll
+          for (int o = 0; o < T; ++o) acc[r][o] = fma4(acc[r][o], row[o * S + tx], f);
+        }
       }
     }
-    float* yb = y + (((long)img * g.oh + oy) * g.ow) * g.c + 4 * q;
 #pragma unroll
-    for (int o = 0; o < T; ++o)
-      if (ox0 + o < g.ow) *reinterpret_cast<float4*>(yb + (long)(ox0 + o) * g.c) = acc[o];
+    for (int r = 0; r < R; ++r) {
+      if (oy0 + r >= g.oh) break;
+      float* yb = y + (((long)img * g.oh + oy0 + r) * g.ow) * g.c + 4 * q;
+#pragma unroll
+      for (int o = 0; o < T; ++o)
+        if (ox0 + o < g.ow) *reinterpret_cast<float4*>(yb + (long)(ox0 + o) * g.c) = acc[r][o];
+    }
   }
 }
 
-// input gradient, stride 1: dx[iy][ix] = sum dy[iy+pt-ty][ix+pl-tx] w[ty][tx]; T columns per
-// thread from a T+K-1 column window of dy
-template <int K, int T>
+// input gradient, stride 1: dx[iy][ix] = sum dy[iy+pt-ty][ix+pl-tx] w[ty][tx]; a thread owns
+// R rows x T columns of dx from an (R+K-1) x (T+K-1) window of dy, each dy row loaded once. dy
+// rows are visited bottom-up so every output still sums its taps in ascending (ty, tx) order.
+template <int K, int T, int R>
 __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __restrict__ dy,
                                                               const float* __restrict__ wt,
                                                               DwGeom g, float* __restrict__ dx,
                                                               int accum) {
   constexpr int NC = T + K - 1;
+  constexpr int NR = R + K - 1;
   const int cv = g.c / 4;
   const int tiles = (g.w + T - 1) / T;
-  const int total = g.n * g.h * tiles * cv;
+  const int rgroups = (g.h + R - 1) / R;
+  const int total = g.n * rgroups * tiles * cv;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int t0 = (int)g.dCV.div((uint32_t)e);
     const int q = e - t0 * cv;
     const int t1 = (int)g.dTiles.div((uint32_t)t0);
     const int ix0 = (t0 - t1 * tiles) * T;
     const int img = (int)g.dRows.div((uint32_t)t1);
-    const int iy = t1 - img * g.h;
-    float4 acc[T];
+    const int iy0 = (t1 - img * rgroups) * R;
+    float4 acc[R][T];
 #pragma unroll
-    for (int o = 0; o < T; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int o = 0; o < T; ++o) acc[r][o] = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* db = dy + (long)img * g.oh * g.ow * g.c + 4 * q;
     const int ox_lo = ix0 + g.pl - (K - 1);
+    const int oy_lo = iy0 + g.pt - (K - 1);
 #pragma unroll
-    for (int ty = 0; ty < K; ++ty) {
-      const int oy = iy + g.pt - ty;
+    for (int jr = NR - 1; jr >= 0; --jr) {
+      const int oy = oy_lo + jr;
       if (oy < 0 || oy >= g.oh) continue;
       float4 row[NC];
 #pragma unroll
@@ -134,25 +162,35 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __res
                      ? *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+      const float* wq = wt + 4 * q;
 #pragma unroll
-      for (int tx = 0; tx < K; ++tx) {
-        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
-        // output o uses dy column ix0 + o + pl - tx = ox_lo + (o + K - 1 - tx)
+      for (int r = 0; r < R; ++r) {
+        const int ty = r + K - 1 - jr;  // dx row iy0 + r reads dy row iy0 + r + pt - ty
+        if (ty < 0 || ty >= K) continue;
 #pragma unroll
-        for (int o = 0; o < T; ++o) acc[o] = fma4(acc[o], row[o + K - 1 - tx], f);
+        for (int tx = 0; tx < K; ++tx) {
+          const float4 f = *reinterpret_cast<const float4*>(wq + (ty * K + tx) * g.c);
+          // output o uses dy column ix0 + o + pl - tx = ox_lo + (o + K - 1 - tx)
+#pragma unroll
+          for (int o = 0; o < T; ++o) acc[r][o] = fma4(acc[r][o], row[o + K - 1 - tx], f);
+        }
       }
     }
-    float* xb = dx + (((long)img * g.h + iy) * g.w) * g.c + 4 * q;
 #pragma unroll
-    for (int o = 0; o < T; ++o) {
-      if (ix0 + o >= g.w) continue;
-      float4* d = reinterpret_cast<float4*>(xb + (long)(ix0 + o) * g.c);
-      float4 v = acc[o];
-      if (accum) {
-        const float4 old = *d;
-        v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+    for (int r = 0; r < R; ++r) {
+      if (iy0 + r >= g.h) break;
+      float* xb = dx + (((long)img * g.h + iy0 + r) * g.w) * g.c + 4 * q;
+#pragma unroll
+      for (int o = 0; o < T; ++o) {
+        if (ix0 + o >= g.w) continue;
+        float4* d = reinterpret_cast<float4*>(xb + (long)(ix0 + o) * g.c);
+        float4 v = acc[r][o];
+        if (accum) {
+          const float4 old = *d;
+          v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+        }
+        *d = v;
       }
-      *d = v;
     }
   }
 }
@@ -391,13 +429,18 @@ static DwGeom dw_geom(int n, int h, int w, int c, int s, int pt, int pl, int oh,
   return g;
 }
 
-template <int K, int S, int T>
+template <int K, int S, int T, int R>
 static void dw_fwd_launch(const float* x, const float* wdw, DwGeom& g, float* y, hipStream_t st) {
+  const int rgroups = (g.oh + R - 1) / R;
   g.dTiles = FastDiv((uint32_t)((g.ow + T - 1) / T));
-  g.dRows = FastDiv((uint32_t)g.oh);
-  const long total = (long)g.n * g.oh * ((g.ow + T - 1) / T) * (g.c / 4);
-  if (g.mean) dwconv_fwd_kernel<K, S, T, true><<<grid_for(total), 256, 0, st>>>(x, wdw, g, y);
-  else dwconv_fwd_kernel<K, S, T, false><<<grid_for(total), 256, 0, st>>>(x, wdw, g, y);
+  g.dRows = FastDiv((uint32_t)rgroups);
+  const long total = (long)g.n * rgroups * ((g.ow + T - 1) / T) * (g.c / 4);
+  const unsigned grid = grid_for(total);
+  if (!g.mean) dwconv_fwd_kernel<K, S, T, R, PRO_NONE><<<grid, 256, 0, st>>>(x, wdw, g, y);
+  else if (g.act == ACT_SWISH) dwconv_fwd_kernel<K, S, T, R, ACT_SWISH><<<grid, 256, 0, st>>>(x, wdw, g, y);
+  else if (g.act == ACT_RELU) dwconv_fwd_kernel<K, S, T, R, ACT_RELU><<<grid, 256, 0, st>>>(x, wdw, g, y);
+  else if (g.act == ACT_SIGMOID) dwconv_fwd_kernel<K, S, T, R, ACT_SIGMOID><<<grid, 256, 0, st>>>(x, wdw, g, y);
+  else dwconv_fwd_kernel<K, S, T, R, ACT_NONE><<<grid, 256, 0, st>>>(x, wdw, g, y);
 }
 
 extern "C" int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, const float* wdw,
@@ -414,10 +457,10 @@ extern "C" int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, con
   DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
   g.mean = mean; g.invstd = invstd; g.gamma = gamma; g.beta = beta; g.act = act;
   hipStream_t st = as_stream(stream);
-  if (k == 3 && s == 1) dw_fwd_launch<3, 1, 4>(x, wdw, g, y, st);
-  else if (k == 3) dw_fwd_launch<3, 2, 2>(x, wdw, g, y, st);
-  else if (k == 5 && s == 1) dw_fwd_launch<5, 1, 4>(x, wdw, g, y, st);
-  else if (k == 5) dw_fwd_launch<5, 2, 2>(x, wdw, g, y, st);
+  if (k == 3 && s == 1) dw_fwd_launch<3, 1, 4, 4>(x, wdw, g, y, st);
+  else if (k == 3) dw_fwd_launch<3, 2, 2, 4>(x, wdw, g, y, st);
+  else if (k == 5 && s == 1) dw_fwd_launch<5, 1, 4, 4>(x, wdw, g, y, st);
+  else if (k == 5) dw_fwd_launch<5, 2, 2, 4>(x, wdw, g, y, st);
   else {
     set_error("pld_dwconv_fwd: kernel size %d unsupported (3, 5)", k);
     return PLD_ERR_UNSUPPORTED;
@@ -445,13 +488,15 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
   g.dRows = FastDiv((uint32_t)h);
   hipStream_t st = as_stream(stream);
   if (s == 1) {
-    constexpr int T = 4;
+    constexpr int T = 4, R = 4;
+    const int rgroups = (h + R - 1) / R;
+    g.dRows = FastDiv((uint32_t)rgroups);
     g.dTiles = FastDiv((uint32_t)((w + T - 1) / T));
-    const long total = (long)n * h * ((w + T - 1) / T) * (c / 4);
+    const long total = (long)n * rgroups * ((w + T - 1) / T) * (c / 4);
     if (k == 3)
-      dwconv_dgrad_s1_kernel<3, T><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+      dwconv_dgrad_s1_kernel<3, T, R><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
     else
-      dwconv_dgrad_s1_kernel<5, T><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+      dwconv_dgrad_s1_kernel<5, T, R><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
   } else {
     g.dTiles = FastDiv((uint32_t)w);
     const long total = (long)n * h * w * (c / 4);
