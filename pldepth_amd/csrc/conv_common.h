@@ -31,6 +31,12 @@ struct GemmConvParams {
   long zstride;
   int ktiles_per_split;
   FastDiv dC, dKW, dOW, dOH;
+  // bf16x3 FWD/DGRAD K-step order: 0 = linear in k = (tap, ci); > 0 = tap-inner, K-step
+  // (chunk, tap) covers 32 channels of ONE source at one tap: kc1 = ceil(c1/32) chunks of x1,
+  // then ceil(c2/32) of x2 (kc_tap in all) — one load per element instead of one per source,
+  // and consecutive steps re-read the same channels at shifted taps (L2 hits)
+  int kc_tap, kc1;
+  FastDiv dTaps;
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));

@@ -650,6 +650,7 @@ static int fill_geom(const pld_conv_args* a, GemmConvParams& p) {
   p.dKW = FastDiv((uint32_t)p.kw);
   p.dOW = FastDiv((uint32_t)p.ow);
   p.dOH = FastDiv((uint32_t)p.oh);
+  p.dTaps = FastDiv((uint32_t)(p.kh * p.kw));
   return PLD_OK;
 }
 
@@ -728,12 +729,25 @@ static int x3_choose(long M, long N, long K, int requested, bool wgrad) {
   return best;
 }
 
-static void x3_fwd_plan(long M, long N, long K, int tile, int& cfg, int& splits, int& kt_per) {
+// K-step order of a bf16x3 FWD/DGRAD GEMM (GemmConvParams::kc_tap): tap-inner when a tap spans
+// several 32-channel chunks (im2col re-reads then land in L2 one step apart instead of C/32 steps)
+static int x3_kc_tap(int taps, int c1, int c2) {
+  static const int mode = [] {
+    const char* e = std::getenv("PLD_X3_TAP_INNER");
+    return e ? std::atoi(e) : 1;
+  }();
+  return (mode && taps > 1 && c1 + c2 >= 64) ? (int)(cdiv(c1, X3_BK) + cdiv(c2, X3_BK)) : 0;
+}
+static long x3_ktiles(int kc_tap, int taps, long K) {
+  return kc_tap ? (long)kc_tap * taps : (K + X3_BK - 1) / X3_BK;
+}
+
+static void x3_fwd_plan(long M, long N, long K, long ktiles, int tile, int& cfg, int& splits,
+                        int& kt_per) {
   cfg = x3_choose(M, N, K, tile, false);
   const bool allow = tile >= pld__x3_num_cfg();
   int bm, bn, tm, tn, occ;
   pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
-  const long ktiles = (K + X3_BK - 1) / X3_BK;
   const long blocks = (long)cdiv(M, bm) * cdiv(N, bn);
   long s = 1;
   if (allow) {
@@ -789,7 +803,9 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
       if (rc) return rc;
       p.bsplit = wsp;
     }
-    x3_fwd_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
+    p.kc_tap = x3_kc_tap(p.kh * p.kw, p.c1, p.c2);
+    p.kc1 = (int)cdiv(p.c1, X3_BK);
+    x3_fwd_plan(p.M, p.N, p.K, x3_ktiles(p.kc_tap, p.kh * p.kw, p.K), tile, cfg, splits, kt_per);
     int bm, bn, tm, tn, occ;
     pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
     PLD_CHECK_ARG(fwd_span_bytes(p, bm) < MAX_RECORDS && (long)p.N * p.K * 4 < MAX_RECORDS,
@@ -833,12 +849,13 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   return check_launch("splitk_out_kernel");
 }
 
-static size_t fwd_ws_bytes(long M, long N, long K, int tile, int math = 0, bool geom = false,
-                           bool have_split = true) {
+static size_t fwd_ws_bytes(long M, long N, long K, int taps, int c1, int c2, int tile,
+                           int math = 0, bool geom = false, bool have_split = true) {
   int cfg, splits, kt_per;
   bool x3;
   resolve_sched(math, geom, tile, x3, tile);
-  if (x3) x3_fwd_plan(M, N, K, tile, cfg, splits, kt_per);
+  if (x3)
+    x3_fwd_plan(M, N, K, x3_ktiles(x3_kc_tap(taps, c1, c2), taps, K), tile, cfg, splits, kt_per);
   else fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
   size_t b = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
   if (x3 && !have_split) b = (b + 255) / 256 * 256 + x3_split_bytes(N, K);
@@ -917,7 +934,8 @@ extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;
   return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
-                      (long)a->kh * a->kw * (a->c1 + a->c2), a->tile, a->math,
+                      (long)a->kh * a->kw * (a->c1 + a->c2), a->kh * a->kw, a->c1, a->c2, a->tile,
+                      a->math,
                       x3_fwd_geom(a->c1 + a->c2, a->c1, a->in_scale != nullptr, a->kh * a->kw),
                       a->w_split != nullptr);
 }
@@ -933,9 +951,10 @@ extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
   const bool hs = a->w_split != nullptr;
   if (a->sh != 1 || a->sw != 1)  // 1x1 strided: GEMM into a compact tmp, then scatter
     return strided_tmp_bytes(a) + fwd_ws_bytes((long)a->n * a->oh * a->ow, a->c1 + a->c2,
-                                               a->cout, a->tile, a->math, geom, hs);
+                                               a->cout, 1, a->cout, 0, a->tile, a->math, geom,
+                                               hs);
   return fwd_ws_bytes((long)a->n * a->h * a->w, a->c1 + a->c2, (long)a->kh * a->kw * a->cout,
-                      a->tile, a->math, geom, hs);
+                      a->kh * a->kw, a->cout, 0, a->tile, a->math, geom, hs);
 }
 
 extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,

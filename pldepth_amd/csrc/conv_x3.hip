@@ -131,7 +131,7 @@ struct X3Smem {
 // the same, unconditional set of loads (the concat's second source is a template parameter, the
 // last steps re-fetch the final tile), so the compiler can count the loads in flight and wait
 // for exactly one stage (vmcnt(N)), never draining the prefetch (vmcnt(0)).
-template <int BM, int BN, int MODE, bool CAT>
+template <int BM, int BN, int MODE, bool CAT, bool TI>
 __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned char* smem,
                                             int kt_begin, int kt_end, int pw, int lane, int mb,
                                             int nb) {
@@ -234,7 +234,32 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
 
   auto load_tile = [&](int kt, Stage& st) {
     const int k0 = kt * BK;
-    if (MODE == MODE_FWD) {
+    if (MODE == MODE_FWD && TI) {
+      // tap-inner order: K-step kt = (chunk kq, tap) with the chunks of x1 first, then x2, each
+      // 32 channels of ONE source (ragged last chunk masked): one load per element and the
+      // source's descriptor picked per step (wave-uniform), where the linear order needs both
+      const int kq = (int)p.dTaps.div((uint32_t)kt);
+      const int tap = kt - kq * p.kh * p.kw;
+      const bool s2 = CAT && kq >= p.kc1;
+      const int chb = (s2 ? kq - p.kc1 : kq) * BK;  // first channel of the chunk in its source
+      const int cs = s2 ? p.c2 : p.c1;
+      const __amdgpu_buffer_rsrc_t rs = s2 ? rs2 : rs1;
+      const int c = chb + 4 * ks;
+      const bool kin = c < cs;
+      const int ty = (int)p.dKW.div((uint32_t)tap);
+      const int toff = ty * p.w + (tap - ty * p.kw);  // pixel offset of the tap
+#pragma unroll
+      for (int j = 0; j < FA; ++j) {
+        const bool ok = kin && ((a_taps[j] >> tap) & 1u);
+        st.ra[j] = bload4(rs, ok ? (unsigned)(((a_base[j] + toff) * cs + c) * 4) : OOB);
+      }
+      const int cb8 = chb + 8 * (br & 3);  // this lane's 8-k chunk of the filter
+      const int kc = tap * p.C + (s2 ? p.c1 : 0) + cb8;
+      const bool kcin = cb8 < cs;
+#pragma unroll
+      for (int j = 0; j < FB; ++j)
+        st.rb[j] = bload4(rsb, (b_ok[j] && kcin) ? b_off[j] + 4u * (unsigned)kc : OOB);
+    } else if (MODE == MODE_FWD) {
       const int k = k0 + 4 * ks;  // this lane's 4 consecutive k (C % 8 == 0: one tap, one source)
       const bool kin = k < p.K;
       const int kk = kin ? k : 0;
@@ -446,7 +471,7 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
 // 512 threads: waves 0-3 consume (LDS fragments -> MFMA), waves 4-7 produce the next K-step
 // (global loads, prologue, hi/lo split, LDS stores) — a VALU-heavy wave and an MFMA-heavy
 // wave share each SIMD, so the split overlaps the matrix work.
-template <int BM, int BN, int WM, int WN, int MODE, bool CAT>
+template <int BM, int BN, int WM, int WN, int MODE, bool CAT, bool TI>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvParams p) {
   static_assert(WM * WN == 4, "4 consumer waves");
   static_assert((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
@@ -466,13 +491,13 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvPar
   const int nb = wid % nnb;
   const int mb = (wid / nnb) % nmb;
   const int zb = wid / (nnb * nmb);
-  int kt_begin = 0, kt_end = (p.K + BK - 1) / BK;
+  int kt_begin = 0, kt_end = p.kc_tap ? p.kc_tap * p.kh * p.kw : (p.K + BK - 1) / BK;
   if (p.ktiles_per_split > 0) {
     kt_begin = zb * p.ktiles_per_split;
     kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
   }
   if (wave >= WM * WN)
-    x3_producer<BM, BN, MODE, CAT>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb, nb);
+    x3_producer<BM, BN, MODE, CAT, TI>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb, nb);
   else
     x3_consumer<BM, BN, WM, WN, MODE>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
 }
@@ -491,8 +516,14 @@ constexpr int kNumCfg = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(GemmConvParams& p, int splits, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
-  if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
-  else conv_x3_kernel<BM, BN, WM, WN, MODE, false><<<grid, (WM * WN + 4) * 64, 0, st>>>(p);
+  constexpr int T = (WM * WN + 4) * 64;
+  if (MODE == MODE_FWD && p.kc_tap) {
+    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true, true><<<grid, T, 0, st>>>(p);
+    else conv_x3_kernel<BM, BN, WM, WN, MODE, false, true><<<grid, T, 0, st>>>(p);
+  } else {
+    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true, false><<<grid, T, 0, st>>>(p);
+    else conv_x3_kernel<BM, BN, WM, WN, MODE, false, false><<<grid, T, 0, st>>>(p);
+  }
 }
 
 template <int MODE>
