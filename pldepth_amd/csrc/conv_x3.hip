@@ -187,6 +187,8 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
                 "WGRAD tile columns must be 32..256");
   int w_ty = 0, w_tx = 0, w_ci = 0;
   bool w_ok = false, w_in1 = true;
+  int w_cs = 0;                // WGRAD concat: this thread's source channel count and
+  const float* w_src = p.x1;   // its first channel's address in the workgroup's first image
 
   if (MODE == MODE_FWD) {
 #pragma unroll
@@ -224,6 +226,9 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
     w_ty = (int)ty;
     w_tx = (int)tap - (int)ty * p.kw;
     w_in1 = w_ci < p.c1;
+    w_cs = w_in1 ? p.c1 : p.c2;
+    w_src = w_in1 ? p.x1 + img_base * img_elems * p.c1 + w_ci
+                  : p.x2 + img_base * img_elems * p.c2 + (w_ci - p.c1);
   }
 
   constexpr int RA = (MODE == MODE_FWD) ? FA : 4 * PA;  // float4 staging registers, A
@@ -300,15 +305,18 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
         const int iy = oy * p.sh - p.pt + w_ty, ix = ox * p.sw - p.pl + w_tx;
         const bool ok = rok && w_ok && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
         const int px = (ir + iy) * p.w + ix;
-        const unsigned o1 = (ok && w_in1) ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB;
-        const unsigned o2 = (CAT && ok && !w_in1) ? (unsigned)((px * p.c2 + w_ci - p.c1) * 4) : OOB;
+        if (CAT) {  // this thread's source is fixed: one (per-lane address) load per element;
+                    // masked lanes re-read their first 16 channels and zero the data
+          const float4* a = reinterpret_cast<const float4*>(w_src + (ok ? px * w_cs : 0));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (CAT)
-            st.ra[4 * j + u] = add4(bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u),
-                                    bload4(rs2, o2 == OOB ? OOB : o2 + 16 * u));
-          else
-            st.ra[4 * j + u] = bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u);
+          for (int u = 0; u < 4; ++u) {
+            const float4 v = a[u];
+            st.ra[4 * j + u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        } else {
+          const unsigned o1 = ok ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) st.ra[4 * j + u] = bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u);
         }
       }
       const int gb = ptid / NQB;
