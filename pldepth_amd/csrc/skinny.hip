@@ -14,7 +14,7 @@
 // Algorithmic bytes: fwd/wgrad read x once (+ dy), dgrad writes dx once.
 #include <algorithm>
 
-#include "common.h"
+#include "conv_common.h"
 
 namespace pld {
 
@@ -34,10 +34,35 @@ struct SkinnyParams {
   int tiles_x, tiles_y;
 };
 
+template <int NT>  // workgroup size
 __device__ __forceinline__ void stage_halo(const SkinnyParams& p, float* halo, int img, int y0,
                                            int x0, int c0, int nc) {
   // halo[(hy*HT + hx)*CS + cc] = x[img][y0+hy-pt][x0+hx-pl][c0+cc], zero outside
   const int nq = nc / 4;
+  if (nq == CH / 4) {
+    // full chunk: every load of the halo issued before the first LDS store, through a buffer
+    // descriptor (zeros outside the image) — no branch around a load, so they all overlap
+    constexpr int NQ = CH / 4, TOTAL = HT * HT * NQ;
+    const long img_elems = (long)p.h * p.w * p.c;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.x + img * img_elems, img_elems * 4);
+    constexpr int IT = (TOTAL + NT - 1) / NT;
+    float4 v[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + NT * i;
+      const int q = e % NQ, pix = e / NQ;
+      const int hy = pix / HT, hx = pix % HT;
+      const int iy = y0 + hy - p.pt, ix = x0 + hx - p.pl;
+      const bool ok = e < TOTAL && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+      v[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * p.c + c0 + 4 * q) * 4) : OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + NT * i;
+      if (e < TOTAL) *reinterpret_cast<float4*>(halo + (e / NQ) * CS + 4 * (e % NQ)) = v[i];
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < HT * HT * nq; e += blockDim.x) {
     const int q = e % nq;
     const int pix = e / nq;
@@ -60,7 +85,7 @@ __global__ __launch_bounds__(256) void skinny_fwd_kernel(SkinnyParams p) {
   for (int c0 = 0; c0 < p.c; c0 += CH) {
     const int nc = min(CH, p.c - c0);
     __syncthreads();
-    stage_halo(p, halo, img, y0, x0, c0, nc);
+    stage_halo<256>(p, halo, img, y0, x0, c0, nc);
     for (int e = threadIdx.x; e < 9 * nc; e += blockDim.x)
       wl[(e / nc) * CH + e % nc] = p.wt[(e / nc) * p.c + c0 + e % nc];
     __syncthreads();
@@ -95,33 +120,38 @@ __global__ __launch_bounds__(256) void skinny_dgrad_kernel(SkinnyParams p) {
     dyl[e] = (iy >= 0 && iy < p.h && ix >= 0 && ix < p.w)
                  ? p.dy[((long)img * p.h + iy) * p.w + ix] : 0.f;
   }
-  const int iy = y0 + ty, ix = x0 + tx;
+  (void)tx;
+  (void)ty;
   for (int c0 = 0; c0 < p.c; c0 += 64) {
     const int nc = min(64, p.c - c0);
+    const int nq = nc / 4;
     __syncthreads();
     // p.w is the dgrad-native filter [c][3][3] with flipped taps: W[t][c] = Wd[c][8 - t]
     for (int e = threadIdx.x; e < 9 * nc; e += blockDim.x)
       wl[(e / nc) * 64 + e % nc] = p.wt[(long)(c0 + e % nc) * 9 + (8 - e / nc)];
     __syncthreads();
-    if (iy < p.h && ix < p.w) {
-      float* d = p.y + (((long)img * p.h + iy) * p.w + ix) * p.c + c0;
-      for (int q = 0; q < nc; q += 4) {
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    // one (pixel, 4-channel quad) per thread and pass: neighbouring lanes write neighbouring
+    // 16-byte quads of one pixel, then of the next pixel (full-line stores of the dx rows)
+    for (int e = threadIdx.x; e < ST * ST * nq; e += blockDim.x) {
+      const int q = e % nq, pix = e / nq;
+      const int py = pix / ST, px = pix % ST;
+      const int iy = y0 + py, ix = x0 + px;
+      if (iy >= p.h || ix >= p.w) continue;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          // output (iy - ty + pt) contributes through tap ty: halo row iy-ty+pt-(y0-qt)
-          const int hy = ty + 2 - t / 3, hx = tx + 2 - t % 3;
-          const float g = dyl[hy * HT + hx];
-          const float4 f = *reinterpret_cast<const float4*>(wl + t * 64 + q);
-          a.x += g * f.x; a.y += g * f.y; a.z += g * f.z; a.w += g * f.w;
-        }
-        float4* dp = reinterpret_cast<float4*>(d + q);
-        if (p.acc) {
-          const float4 o = *dp;
-          a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
-        }
-        *dp = a;
+      for (int t = 0; t < 9; ++t) {
+        // output (iy - ty + pt) contributes through tap ty: halo row iy-ty+pt-(y0-qt)
+        const float g = dyl[(py + 2 - t / 3) * HT + px + 2 - t % 3];
+        const float4 f = *reinterpret_cast<const float4*>(wl + t * 64 + 4 * q);
+        a.x += g * f.x; a.y += g * f.y; a.z += g * f.z; a.w += g * f.w;
       }
+      float4* dp = reinterpret_cast<float4*>(p.y + (((long)img * p.h + iy) * p.w + ix) * p.c +
+                                             c0 + 4 * q);
+      if (p.acc) {
+        const float4 o = *dp;
+        a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+      }
+      *dp = a;
     }
   }
 }
@@ -154,7 +184,7 @@ __global__ __launch_bounds__(WG_THREADS) void skinny_wgrad_kernel(SkinnyParams p
       if (k >= nchunks) break;
       const int c0 = k * CH, nc = min(CH, p.c - c0);
       if (k > 0) __syncthreads();
-      stage_halo(p, halo, img, y0, x0, c0, nc);
+      stage_halo<WG_THREADS>(p, halo, img, y0, x0, c0, nc);
       __syncthreads();
       if (e < 9 * nc) {
         const int t = e / nc, cc = e % nc;
