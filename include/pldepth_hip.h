@@ -307,6 +307,20 @@ int pld_sampler_rank(const float* gt, const int* valid_idx, const int* nvalid,
 int pld_sampler_candidates(int R, int strategy); /* int(R * factor) */
 
 /* ------------------------------------------------------------------------------------------
+ * Test-pass metrics, one workgroup per image. Pixel pairs / lists are drawn on
+ * the host exactly as the reference draws them and passed as int32 flat pixel indices.
+ * ------------------------------------------------------------------------------------------ */
+/* pldepth/active_learning/metrics.py:60-70 ordinal_error, for n images of hw pixels:
+ * err[i] = 1 - #{j : (pred[idx0[j]] > pred[idx1[j]]) == (gt[idx0[j]] > gt[idx1[j]])} / num */
+int pld_ordinal_error(const float* pred, const float* gt, int n, int64_t hw, const int32_t* idx0,
+                      const int32_t* idx1, int num, double* err, void* stream);
+/* metrics.py:92-109 calc_d: pred min-max normalised over the image (cv2 NORM_MINMAX to [0,1]),
+ * the list_size (<= 1024) listed pixels of pred and gt sorted ascending, out[i] = DCG(pred) /
+ * DCG(gt) with DCG = sum_k (1 / (v_k + 1)) / log2(k + 2) (metrics.py:83-89 calcDCG) */
+int pld_dcg_ratio(const float* pred, const float* gt, int n, int64_t hw, const int32_t* ids,
+                  int list_size, double* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * hipGraph capture of a whole stream-ordered step (replaces Keras' per-op dispatch)
  * ------------------------------------------------------------------------------------------ */
 int pld_graph_begin(void* stream);

@@ -500,3 +500,25 @@ def sampler_rank(gt, valid_idx, nvalid, gt_minmax, draws, R, L, strategy, out):
     lib().pld_sampler_rank(ptr(gt), ptr(valid_idx), ptr(nvalid), ptr(gt_minmax), ptr(draws), B,
                            H, W, R, L, sid, ptr(out), ptr(ws), stream())
     return out
+
+
+# ---- test-pass metrics (pld_ordinal_error / pld_dcg_ratio) ----
+def ordinal_error(pred, gt, idx0, idx1):
+    """pred, gt: [n, hw] float32 device tensors; idx0/idx1: int32 device indices -> [n] float64."""
+    n, hw = pred.shape[0], pred[0].numel()
+    assert gt.shape[0] == n and gt[0].numel() == hw and idx0.numel() == idx1.numel()
+    assert idx0.dtype == torch.int32 and idx1.dtype == torch.int32
+    out = torch.empty(n, dtype=torch.float64, device=pred.device)
+    lib().pld_ordinal_error(ptr(_f32(pred)), ptr(_f32(gt)), n, hw, ptr(idx0), ptr(idx1),
+                            idx0.numel(), ptr(out), stream())
+    return out
+
+
+def dcg_ratio(pred, gt, ids):
+    """pred, gt: [n, hw] float32 device tensors; ids: int32 device list -> [n] float64."""
+    n, hw = pred.shape[0], pred[0].numel()
+    assert gt.shape[0] == n and gt[0].numel() == hw and ids.dtype == torch.int32
+    out = torch.empty(n, dtype=torch.float64, device=pred.device)
+    lib().pld_dcg_ratio(ptr(_f32(pred)), ptr(_f32(gt)), n, hw, ptr(ids), ids.numel(), ptr(out),
+                        stream())
+    return out
