@@ -34,77 +34,101 @@ struct SkinnyParams {
   int tiles_x, tiles_y;
 };
 
-template <int NT>  // workgroup size
-__device__ __forceinline__ void stage_halo(const SkinnyParams& p, float* halo, int img, int y0,
-                                           int x0, int c0, int nc) {
-  // halo[(hy*HT + hx)*CS + cc] = x[img][y0+hy-pt][x0+hx-pl][c0+cc], zero outside
-  const int nq = nc / 4;
-  if (nq == CH / 4) {
-    // full chunk: every load of the halo issued before the first LDS store, through a buffer
-    // descriptor (zeros outside the image) — no branch around a load, so they all overlap
-    constexpr int NQ = CH / 4, TOTAL = HT * HT * NQ;
-    const long img_elems = (long)p.h * p.w * p.c;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.x + img * img_elems, img_elems * 4);
-    constexpr int IT = (TOTAL + NT - 1) / NT;
-    float4 v[IT];
+constexpr int MAX_C = 2 * CH;  // eligibility bound (ReDWeb's aol/conv1 has 64 input channels)
+constexpr int NT = 256;        // workgroup size of the halo kernels
+
+// One 32-channel chunk of a tile's 18x18 input halo in flight in registers: every load issued
+// at once through a buffer descriptor (zeros outside the image and past the last channel) — no
+// branch around a load — so the next tile's halo streams in while the current one is computed.
+// halo[(hy*HT + hx)*CS + cc] = x[img][y0+hy-pt][x0+hx-pl][c0+cc]
+struct HaloRegs {
+  static constexpr int NQ = CH / 4, TOTAL = HT * HT * NQ, IT = (TOTAL + NT - 1) / NT;
+  float4 v[IT];
+  float dy;  // wgrad: this thread's dy pixel of the tile
+};
+
+__device__ __forceinline__ void tile_origin(const SkinnyParams& p, int tile, int& img, int& y0,
+                                            int& x0) {
+  img = tile / (p.tiles_x * p.tiles_y);
+  const int r = tile - img * p.tiles_x * p.tiles_y;
+  y0 = (r / p.tiles_x) * ST;
+  x0 = (r % p.tiles_x) * ST;
+}
+
+__device__ __forceinline__ void halo_load(const SkinnyParams& p, HaloRegs& h, int tile, int c0,
+                                          bool with_dy) {
+  int img, y0, x0;
+  tile_origin(p, tile, img, y0, x0);
+  const int nc = min(CH, p.c - c0);
+  const int img_elems = p.h * p.w * p.c;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.x + (long)img * img_elems, (long)img_elems * 4);
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int e = threadIdx.x + NT * i;
-      const int q = e % NQ, pix = e / NQ;
-      const int hy = pix / HT, hx = pix % HT;
-      const int iy = y0 + hy - p.pt, ix = x0 + hx - p.pl;
-      const bool ok = e < TOTAL && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-      v[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * p.c + c0 + 4 * q) * 4) : OOB);
-    }
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int e = threadIdx.x + NT * i;
-      if (e < TOTAL) *reinterpret_cast<float4*>(halo + (e / NQ) * CS + 4 * (e % NQ)) = v[i];
-    }
-    return;
-  }
-  for (int e = threadIdx.x; e < HT * HT * nq; e += blockDim.x) {
-    const int q = e % nq;
-    const int pix = e / nq;
+  for (int i = 0; i < HaloRegs::IT; ++i) {
+    const int e = threadIdx.x + NT * i;
+    const int q = e % HaloRegs::NQ, pix = e / HaloRegs::NQ;
     const int hy = pix / HT, hx = pix % HT;
     const int iy = y0 + hy - p.pt, ix = x0 + hx - p.pl;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (iy >= 0 && iy < p.h && ix >= 0 && ix < p.w)
-      v = *reinterpret_cast<const float4*>(p.x + (((long)img * p.h + iy) * p.w + ix) * p.c + c0 +
-                                           4 * q);
-    *reinterpret_cast<float4*>(halo + pix * CS + 4 * q) = v;
+    const bool ok = e < HaloRegs::TOTAL && 4 * q < nc && (unsigned)iy < (unsigned)p.h &&
+                    (unsigned)ix < (unsigned)p.w;
+    h.v[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * p.c + c0 + 4 * q) * 4) : OOB);
+  }
+  if (with_dy) {
+    const int hw = p.h * p.w;
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.dy + (long)img * hw, (long)hw * 4);
+    const int oy = y0 + threadIdx.x / ST, ox = x0 + threadIdx.x % ST;
+    h.dy = bload1(rd, (oy < p.h && ox < p.w) ? (unsigned)((oy * p.w + ox) * 4) : OOB);
   }
 }
 
-__global__ __launch_bounds__(256) void skinny_fwd_kernel(SkinnyParams p) {
-  __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
-  __shared__ __attribute__((aligned(16))) float wl[9 * CH];
-  const int tx = threadIdx.x % ST, ty = threadIdx.x / ST;
-  const int x0 = blockIdx.x * ST, y0 = blockIdx.y * ST, img = blockIdx.z;
-  float acc = 0.f;
-  for (int c0 = 0; c0 < p.c; c0 += CH) {
-    const int nc = min(CH, p.c - c0);
-    __syncthreads();
-    stage_halo<256>(p, halo, img, y0, x0, c0, nc);
-    for (int e = threadIdx.x; e < 9 * nc; e += blockDim.x)
-      wl[(e / nc) * CH + e % nc] = p.wt[(e / nc) * p.c + c0 + e % nc];
-    __syncthreads();
+__device__ __forceinline__ void halo_store(const HaloRegs& h, float* halo) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float* hp = halo + ((ty + t / 3) * HT + tx + t % 3) * CS;
-      const float* wp = wl + t * CH;
-      for (int q = 0; q < nc; q += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(hp + q);
-        const float4 f = *reinterpret_cast<const float4*>(wp + q);
-        acc += v.x * f.x + v.y * f.y + v.z * f.z + v.w * f.w;
+  for (int i = 0; i < HaloRegs::IT; ++i) {
+    const int e = threadIdx.x + NT * i;
+    if (e < HaloRegs::TOTAL)
+      *reinterpret_cast<float4*>(halo + (e / HaloRegs::NQ) * CS + 4 * (e % HaloRegs::NQ)) = h.v[i];
+  }
+}
+
+// persistent workgroups over the tiles; the halo chunk of the next (tile, chunk) stage is loaded
+// before the current one is computed (the index is clamped at the end: a harmless re-load)
+template <int NCH>
+__global__ __launch_bounds__(NT) void skinny_fwd_kernel(SkinnyParams p) {
+  __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
+  __shared__ __attribute__((aligned(16))) float wl[9 * MAX_C];
+  const int tx = threadIdx.x % ST, ty = threadIdx.x / ST;
+  const int ntiles = p.tiles_x * p.tiles_y * p.n;
+  for (int e = threadIdx.x; e < 9 * p.c; e += NT) wl[(e / p.c) * MAX_C + e % p.c] = p.wt[e];
+  HaloRegs hr;
+  halo_load(p, hr, min((int)blockIdx.x, ntiles - 1), 0, false);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      __syncthreads();
+      halo_store(hr, halo);
+      __syncthreads();
+      if (k + 1 < NCH) halo_load(p, hr, tile, (k + 1) * CH, false);
+      else halo_load(p, hr, min(tile + (int)gridDim.x, ntiles - 1), 0, false);
+      const int nc = min(CH, p.c - k * CH);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float* hp = halo + ((ty + t / 3) * HT + tx + t % 3) * CS;
+        const float* wp = wl + t * MAX_C + k * CH;
+        for (int q = 0; q < nc; q += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(hp + q);
+          const float4 f = *reinterpret_cast<const float4*>(wp + q);
+          acc += v.x * f.x + v.y * f.y + v.z * f.z + v.w * f.w;
+        }
       }
     }
-  }
-  const int oy = y0 + ty, ox = x0 + tx;
-  if (oy < p.h && ox < p.w) {
-    float* d = p.y + ((long)img * p.h + oy) * p.w + ox;
-    const float v = acc + (p.bias ? p.bias[0] : 0.f);
-    *d = p.acc ? *d + v : v;
+    int img, y0, x0;
+    tile_origin(p, tile, img, y0, x0);
+    const int oy = y0 + ty, ox = x0 + tx;
+    if (oy < p.h && ox < p.w) {
+      float* d = p.y + ((long)img * p.h + oy) * p.w + ox;
+      const float v = acc + (p.bias ? p.bias[0] : 0.f);
+      *d = p.acc ? *d + v : v;
+    }
   }
 }
 
@@ -156,56 +180,79 @@ __global__ __launch_bounds__(256) void skinny_dgrad_kernel(SkinnyParams p) {
   }
 }
 
-// 576 threads = 2 pixel halves x 288 (tap, channel) pairs: every thread does equal work
-constexpr int WG_THREADS = 576;
-
-constexpr int MAX_C = 2 * CH;  // eligibility bound (ReDWeb's aol/conv1 has 64 input channels)
-
-__global__ __launch_bounds__(WG_THREADS) void skinny_wgrad_kernel(SkinnyParams p) {
+// 256 threads = 8 channel quads x 32 pixel groups of 8 pixels: per pixel a thread reads dy once
+// and the 9 tap quads of its halo column, 4 FMAs per 16-byte LDS read; persistent workgroups
+// over a strided set of tiles with the next halo chunk in flight during the current one's
+// compute. Groups are combined by a fixed shuffle tree inside each wave, then across the 4 waves
+// in LDS (deterministic).
+template <int NCH>
+__global__ __launch_bounds__(NT) void skinny_wgrad_kernel(SkinnyParams p) {
   __shared__ __attribute__((aligned(16))) float halo[HT * HT * CS];
   __shared__ float dyl[ST * ST];
-  __shared__ float comb[9 * MAX_C];
+  __shared__ __attribute__((aligned(16))) float comb[4][9 * MAX_C];
   const int ntiles = p.tiles_x * p.tiles_y * p.n;
-  const int half = threadIdx.x / (9 * CH);
-  const int e = threadIdx.x % (9 * CH);
-  const int nchunks = (p.c + CH - 1) / CH;
-  float acc[MAX_C / CH] = {0.f, 0.f};
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int img = tile / (p.tiles_x * p.tiles_y);
-    const int r = tile % (p.tiles_x * p.tiles_y);
-    const int y0 = (r / p.tiles_x) * ST, x0 = (r % p.tiles_x) * ST;
-    __syncthreads();
-    if (threadIdx.x < ST * ST) {
-      const int oy = y0 + threadIdx.x / ST, ox = x0 + threadIdx.x % ST;
-      dyl[threadIdx.x] = (oy < p.h && ox < p.w) ? p.dy[((long)img * p.h + oy) * p.w + ox] : 0.f;
-    }
+  const int q = threadIdx.x & 7, pg = threadIdx.x >> 3;
+  float4 acc[NCH][9];
 #pragma unroll
-    for (int k = 0; k < MAX_C / CH; ++k) {
-      if (k >= nchunks) break;
-      const int c0 = k * CH, nc = min(CH, p.c - c0);
-      if (k > 0) __syncthreads();
-      stage_halo<WG_THREADS>(p, halo, img, y0, x0, c0, nc);
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[k][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  HaloRegs hr;
+  halo_load(p, hr, min((int)blockIdx.x, ntiles - 1), 0, true);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
       __syncthreads();
-      if (e < 9 * nc) {
-        const int t = e / nc, cc = e % nc;
-        const float* hp = halo + ((t / 3) * HT + t % 3) * CS + cc;
-        float s = 0.f;
-        for (int py = half * (ST / 2); py < (half + 1) * (ST / 2); ++py)
-#pragma unroll 8
-          for (int px = 0; px < ST; ++px) s += hp[(py * HT + px) * CS] * dyl[py * ST + px];
-        acc[k] += s;
+      halo_store(hr, halo);
+      if (k == 0) dyl[threadIdx.x] = hr.dy;
+      __syncthreads();
+      if (k + 1 < NCH) halo_load(p, hr, tile, (k + 1) * CH, false);
+      else halo_load(p, hr, min(tile + (int)gridDim.x, ntiles - 1), 0, true);
+      if (4 * q < min(CH, p.c - k * CH)) {
+#pragma unroll 2
+        for (int i = 0; i < 8; ++i) {
+          const int pix = pg * 8 + i, py = pix / ST, px = pix % ST;
+          const float g = dyl[pix];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(
+                halo + ((py + t / 3) * HT + px + t % 3) * CS + 4 * q);
+            acc[k][t].x += v.x * g;
+            acc[k][t].y += v.y * g;
+            acc[k][t].z += v.z * g;
+            acc[k][t].w += v.w * g;
+          }
+        }
       }
     }
   }
-  // combine the two pixel halves; partial index = tap * c + channel (HWIO with cout 1)
-  for (int k = 0; k < nchunks; ++k) {
-    const int c0 = k * CH, nc = min(CH, p.c - c0);
-    const bool act = e < 9 * nc;
-    const int o = act ? (e / nc) * p.c + c0 + e % nc : 0;
-    __syncthreads();
-    if (half == 1 && act) comb[o] = acc[k];
-    __syncthreads();
-    if (half == 0 && act) p.part[(long)blockIdx.x * 9 * p.c + o] = acc[k] + comb[o];
+  // reduce the 8 pixel groups of each wave (lane bits 3..5), then the 4 waves
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        acc[k][t].x += __shfl_xor(acc[k][t].x, o);
+        acc[k][t].y += __shfl_xor(acc[k][t].y, o);
+        acc[k][t].z += __shfl_xor(acc[k][t].z, o);
+        acc[k][t].w += __shfl_xor(acc[k][t].w, o);
+      }
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    if (lane < 8 && 4 * lane < min(CH, p.c - k * CH)) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        *reinterpret_cast<float4*>(&comb[wave][t * MAX_C + k * CH + 4 * lane]) = acc[k][t];
+    }
+  }
+  __syncthreads();
+  // partial index = tap * c + channel (HWIO with cout 1)
+  for (int e = threadIdx.x; e < 9 * p.c; e += NT) {
+    const int t = e / p.c, c = e - t * p.c;
+    const int o = t * MAX_C + c;
+    p.part[(long)blockIdx.x * 9 * p.c + e] = ((comb[0][o] + comb[1][o]) + comb[2][o]) + comb[3][o];
   }
 }
 
@@ -228,6 +275,7 @@ __global__ __launch_bounds__(256) void skinny_wgrad_reduce_kernel(const float* _
 }
 
 constexpr int SKINNY_WG_BLOCKS = 2048;
+constexpr int SKINNY_FWD_BLOCKS = 2048;  // persistent: ~3 per CU, each over a strided tile set
 
 }  // namespace pld
 
@@ -258,8 +306,10 @@ extern "C" int pld__skinny_fwd(const pld_conv_args* a, const float* w_ohwi, cons
   p.bias = bias;
   p.y = y;
   p.acc = accumulate;
-  dim3 grid(p.tiles_x, p.tiles_y, p.n);
-  skinny_fwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(p);
+  const int ntiles = p.tiles_x * p.tiles_y * p.n;
+  const int nb = std::min(SKINNY_FWD_BLOCKS, ntiles);
+  if (p.c > CH) skinny_fwd_kernel<2><<<nb, NT, 0, as_stream(stream)>>>(p);
+  else skinny_fwd_kernel<1><<<nb, NT, 0, as_stream(stream)>>>(p);
   return check_launch("skinny_fwd_kernel");
 }
 
@@ -287,7 +337,8 @@ extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float*
   const int ntiles = p.tiles_x * p.tiles_y * p.n;
   const int nb = std::min(SKINNY_WG_BLOCKS, ntiles);
   hipStream_t st = as_stream(stream);
-  skinny_wgrad_kernel<<<nb, WG_THREADS, 0, st>>>(p);
+  if (p.c > CH) skinny_wgrad_kernel<2><<<nb, NT, 0, st>>>(p);
+  else skinny_wgrad_kernel<1><<<nb, NT, 0, st>>>(p);
   int rc = check_launch("skinny_wgrad_kernel");
   if (rc) return rc;
   const int per = 9 * p.c;

@@ -100,6 +100,8 @@ CONV_CASES = [
     (1, 10, 10, 12, 0, 3, 1, 1, True, False),      # Cout=1, C not a multiple of 8
     (2, 20, 18, 64, 0, 3, 1, 1, True, False),      # Cout=1, 64 channels (ReDWeb aol/conv1)
     (1, 17, 33, 36, 0, 3, 1, 1, False, False),     # Cout=1, ragged second channel chunk
+    (16, 200, 200, 32, 0, 3, 1, 1, True, False),   # Cout=1, > 2048 tiles: persistent blocks
+    (24, 150, 150, 36, 0, 3, 1, 1, False, False),  #   loop over several tiles (+ 2 chunks)
     (2, 12, 12, 48, 48, 3, 1, 144, True, False),   # N=144 (128x160 tile), dgrad N=96
     (1, 9, 9, 32, 64, 3, 1, 240, True, False),     # N=240; dgrad splits 32|64
     (1, 8, 8, 96, 0, 3, 1, 224, True, False),      # N=224 exact tile
