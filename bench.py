@@ -218,9 +218,10 @@ def main():
                     help="ff_redweb = the ResNet-50 backbone (BASELINE cfg3 'ff_resnet')")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--conv-math", default="mixed", choices=["mixed", "bf16x3", "fp32"],
-                    help="conv arithmetic policy (kernels.conv_policy): mixed = encoder fp32, "
-                         "decoder bf16x3")
+    ap.add_argument("--conv-math", default="auto", choices=["auto", "mixed", "bf16x3", "fp32"],
+                    help="conv arithmetic policy (kernels.conv_policy): auto = decoder bf16x3, "
+                         "encoder bf16x3 where the BN sees >= 4096 values per channel (all of "
+                         "them at 448x448 batch 32); mixed = encoder fp32, decoder bf16x3")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "conv_traffic.json"),
                     help="PMC traffic summary of the conv family (tools/traffic.py --json)")
     ap.add_argument("--tile-cache", default="",

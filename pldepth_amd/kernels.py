@@ -123,8 +123,13 @@ def same_pads(h, k, s):
 # holds ~83 % of the conv FLOPs; "bf16x3" / "fp32" use one arithmetic everywhere.
 # PLD_CONV_MATH overrides the default policy.
 MATH = {"fp32": 0, "bf16x3": 1}
-POLICIES = ("mixed", "bf16x3", "fp32")
-CONV_MATH = [os.environ.get("PLD_CONV_MATH", "mixed")]
+# conv arithmetic policies: "auto" (default) = decoder bf16x3, encoder bf16x3
+# where the BN after the conv normalises over >= X3_MIN_POPULATION values per channel, exact
+# fp32 below (BN over a handful of pixels amplifies any rounding); "mixed" = encoder fp32,
+# decoder bf16x3; "bf16x3" / "fp32" everywhere
+POLICIES = ("auto", "mixed", "bf16x3", "fp32")
+X3_MIN_POPULATION = 4096
+CONV_MATH = [os.environ.get("PLD_CONV_MATH", "auto")]
 
 
 def set_conv_math(policy):
@@ -139,7 +144,19 @@ def conv_policy(policy=None):
     policy = policy or CONV_MATH[0]
     if policy not in POLICIES:
         raise ValueError(f"conv math must be one of {POLICIES}, got {policy!r}")
-    return ("fp32", "bf16x3") if policy == "mixed" else (policy, policy)
+    if policy == "mixed":
+        return ("fp32", "bf16x3")
+    if policy == "auto":
+        return ("auto", "bf16x3")
+    return (policy, policy)
+
+
+def encoder_math(enc_math, population):
+    """Resolve an engine's encoder math for one conv whose BN sees `population` values per
+    channel (batch x output pixels)."""
+    if enc_math != "auto":
+        return enc_math
+    return "bf16x3" if population >= X3_MIN_POPULATION else "fp32"
 
 
 def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None, in_shift=None,

@@ -282,6 +282,10 @@ class EffNetFF:
         return self._gpre[key]
 
     # ------------------------------------------------------------------ forward
+    def _em(self, oh, ow):
+        """Encoder conv math for a conv with an oh x ow output (its BN sees B*oh*ow values)."""
+        return K.encoder_math(self.enc_math, self.B * oh * ow)
+
     def forward(self, training=True, step=0, image_offset=0):
         """step: int or device int64 tensor (drop-connect Philox counter); image_offset: global
         index of this replica's first image (draws independent of the GPU count)."""
@@ -295,7 +299,7 @@ class EffNetFF:
         x = A["input"]
         h, w = self.H // 2, self.W // 2
         args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none",
-                 math=self.enc_math)
+                 math=self._em(h, w))
         K.conv2d_fwd(args, self.stem.w_nat, None, A["stem_pre"])
         rows = B * h * w
         self.stem_bn.stats_(A["stem_pre"], rows, training)
@@ -305,7 +309,7 @@ class EffNetFF:
             x = self._block_fwd(blk, x, training, step, li)
         h, w = x.shape[1], x.shape[2]
         rows = B * h * w
-        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280, math=self.enc_math), self.top.w_nat,
+        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280, math=self._em(h, w)), self.top.w_nat,
                      None, A["top_pre"])
         self.top_bn.stats_(A["top_pre"], rows, training)
         self.top_bn.apply(A["top_pre"], rows, "swish", A["top_activation"], training)
@@ -332,7 +336,8 @@ class EffNetFF:
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
         pt, pl = blk["pad"]
         if blk["ex"] != 1:
-            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"], math=self.enc_math),
+            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
+                                     math=self._em(h, w)),
                          blk["expand"].w_nat, None, A[n + "expand_pre"])
             ebn = blk["expand_bn"]
             ebn.stats_(A[n + "expand_pre"], B * h * w, training)
@@ -363,7 +368,7 @@ class EffNetFF:
         else:
             self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
         K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
-                                 math=self.enc_math),
+                                 math=self._em(oh, ow)),
                      blk["project"].w_nat, None, A[n + "project_pre"])
         pbn = blk["project_bn"]
         pbn.stats_(A[n + "project_pre"], rows, training)
@@ -431,7 +436,7 @@ class EffNetFF:
         gpre = self._gpre_buf(A["top_pre"].shape)
         self.top_bn.bwd(A["top_pre"], G["top_activation"], rows, "swish", gpre)
         last = self.blocks[-1]["name"] + "output"
-        K.conv2d_dgrad(a(A[last], None, 1, 1, 1, 0, 0, h, w, 1280, math=self.enc_math), gpre,
+        K.conv2d_dgrad(a(A[last], None, 1, 1, 1, 0, 0, h, w, 1280, math=self._em(h, w)), gpre,
                        self.top.w_dg, G[last])
         for bi in range(len(self.blocks) - 1, -1, -1):
             blk = self.blocks[bi]
@@ -459,7 +464,7 @@ class EffNetFF:
         blk["project_bn"].bwd(A[n + "project_pre"], gbn, rows, "none", gp)
         gse = G[n + "se_excite"]
         K.conv2d_dgrad(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
-                                   math=self.enc_math),
+                                   math=self._em(oh, ow)),
                        gp, blk["project"].w_dg, gse)
         F = self.frozen
         K.se_bwd(gse, A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
@@ -477,7 +482,7 @@ class EffNetFF:
             gpe = self._gpre_buf(A[n + "expand_pre"].shape)
             blk["expand_bn"].bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
             K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                       math=self.enc_math), gpe,
+                                       math=self._em(h, w)), gpe,
                            blk["expand"].w_dg, gx_in)
         else:
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)

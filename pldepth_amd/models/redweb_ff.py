@@ -231,8 +231,11 @@ class RedWebFF:
         return self._gpre[key]
 
     # ------------------------------------------------------------------ forward
-    def _math(self, conv):
-        return self.dec_math if conv.trainable else self.enc_math
+    def _math(self, conv, oh=None, ow=None):
+        if conv.trainable:
+            return self.dec_math
+        # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
+        return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1))
 
     def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None):
         """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout]."""
@@ -241,7 +244,8 @@ class RedWebFF:
             pt, pl = (k - 1) // 2, (k - 1) // 2
         else:
             pt = pl = 0
-        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout, math=self._math(conv))
+        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
+                           math=self._math(conv, oh, ow))
         K.conv2d_fwd(args, conv.w_nat, conv.b, y, accumulate=acc)
         return args
 
@@ -250,7 +254,8 @@ class RedWebFF:
         H, W = self.H, self.W
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
-        args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64, math=self.enc_math)
+        args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64,
+                           math=K.encoder_math(self.enc_math, B * h * w))
         K.conv2d_fwd(args, self.stem.w_nat, self.stem.b, A["conv1_pre"])
         self.stem_bn.stats_(A["conv1_pre"], B * h * w, training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
@@ -334,7 +339,8 @@ class RedWebFF:
         """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given."""
         k, s = conv.k, conv.stride
         pt = pl = ((k - 1) // 2 if s == 1 else 0)
-        args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout, math=self._math(conv))
+        args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout,
+                           math=self._math(conv, oh, ow))
         if conv.trainable:
             K.conv2d_wgrad(args, gy, conv.dw)
             if conv.db is not None:

@@ -143,3 +143,29 @@ def test_inference_mode_uses_moving_statistics(step_results, cuda):
     with torch.no_grad():
         ref = forward_infer()
     assert rel(pred, ref) < TOL
+
+
+@pytest.mark.parametrize("policy", ["bf16x3", "auto"])
+def test_forward_448_conv_policy(cuda, policy):
+    """At the benchmark resolution every encoder BN normalises over thousands of values per
+    channel, so bf16x3 convs everywhere (the 'auto' policy's choice at batch 32) stay well inside
+    the 1e-3 bar (measured ~2.5e-4 at the deepest taps); at the 64x64 test size above, BN over a
+    few pixels amplifies rounding and 'auto' keeps those encoder convs exact fp32."""
+    B, H = 2, 448
+    eng = EffNetFF((H, H, 3), B, seed=0, conv_math=policy)
+    eng.drop_connect = False
+    rng = np.random.default_rng(0)
+    x = rng.random((B, H, H, 3)).astype(np.float32)
+    weights = eng.get_weights()
+    eng.act["input"].copy_(torch.from_numpy(x))
+    pred = eng.forward(training=True)
+    torch.cuda.synchronize()
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    taps = {}
+    with torch.no_grad():
+        pred_ref = OE.forward(P, torch.tensor(x, dtype=torch.float64), taps=taps)
+    for name in ["stem_activation", "block2a_output", "block3a_expand_activation",
+                 "block4a_output", "block5c_output", "block7a_output", "top_activation"]:
+        e = rel(eng.act[name], taps[name].permute(0, 2, 3, 1))
+        assert e < TOL, (name, e)
+    assert rel(pred, pred_ref) < TOL

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--model", default="ff_effnet")
     ap.add_argument("--size", type=int, default=448)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--math", nargs="+", default=["mixed", "bf16x3", "fp32"])
+    ap.add_argument("--math", nargs="+", default=["auto", "mixed", "fp32"])
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     import bench
