@@ -307,6 +307,16 @@ int pld_sampler_rank(const float* gt, const int* valid_idx, const int* nvalid,
 int pld_sampler_candidates(int R, int strategy); /* int(R * factor) */
 
 /* ------------------------------------------------------------------------------------------
+ * HR-WSI data access: tf.image.resize of decoded images / depth maps (bilinear)
+ * and validity masks (nearest), TF2 semantics (half-pixel centres, no antialias),
+ * pldepth/data/dao/hr_wsi.py:65-74. NHWC float32 [n][h][w][c] -> [n][oh][ow][c].
+ * ------------------------------------------------------------------------------------------ */
+int pld_resize_bilinear(const float* x, int n, int h, int w, int c, int oh, int ow, float* y,
+                        void* stream);
+int pld_resize_nearest(const float* x, int n, int h, int w, int c, int oh, int ow, float* y,
+                       void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Test-pass metrics, one workgroup per image. Pixel pairs / lists are drawn on
  * the host exactly as the reference draws them and passed as int32 flat pixel indices.
  * ------------------------------------------------------------------------------------------ */

@@ -4,9 +4,9 @@
         --rankings_per_image 100 --epochs 2 --ds_size 256 --input_size 448
 
 Differences from the reference driver, all outside the accelerated path:
-  * data: HR-WSI on-disk decoding is not built yet; ``--data_npz`` loads in-memory arrays
-    (imgs [N,H,W,3] in [0,1], gts [N,H,W], masks [N,H,W]) and without it a seeded synthetic
-    HR-WSI-shaped set is generated;
+  * data: ``--hr_wsi_path`` reads the HR-WSI tree (pldepth_amd.data.dao.hr_wsi: host decode, GPU
+    resize); ``--data_npz`` loads in-memory arrays (imgs [N,H,W,3] in [0,1], gts [N,H,W],
+    masks [N,H,W]); without either a seeded synthetic HR-WSI-shaped set is generated;
   * no wandb / mlflow: metrics go to stdout and ``--log_jsonl``;
   * ``--input_size`` (the reference hard-codes 224 here and 448 in run_scripts/test_sampling.py).
 Everything per step — sampling, forward, ListMLE, backward, Adam-AMSGrad — runs on the GPU.
@@ -82,13 +82,14 @@ class JSONLLogger(object):
 @click.option('--ds_size', default=None, type=click.INT)
 @click.option('--input_size', default=224, type=click.INT)
 @click.option('--data_npz', default='', help='npz with imgs/gts/masks arrays')
+@click.option('--hr_wsi_path', default='', help='HR-WSI root ({train,val}/{imgs,gts,valid_masks})')
 @click.option('--save_path', default='', help='save weights (.npz) after training')
 @click.option('--log_jsonl', default='', help='per-batch metrics file')
 def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_size,
                                rankings_per_image, initial_lr, equality_threshold,
                                model_checkpoints, load_model_path, augmentation, warmup,
                                sampling_type, lr_multi, ds_size, input_size, data_npz, save_path,
-                               log_jsonl):
+                               log_jsonl, hr_wsi_path=''):
     np.random.seed(seed)
     model_params = ModelParameters()
     model_params.set_parameter("model_type", get_model_type_by_name(model_name))
@@ -115,7 +116,12 @@ def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_siz
     shape = [input_size, input_size, 3]
     model, preprocess_fn = get_pl_depth_net(model_params, shape)
 
-    if data_npz:
+    if hr_wsi_path:  # PLDepth.py:100-110: HR-WSI train split, decoded + resized (dao/hr_wsi.py)
+        from .data.dao.hr_wsi import HRWSITFDataAccessObject
+        dao = HRWSITFDataAccessObject(hr_wsi_path, shape, seed)
+        imgs, gts, masks = dao.get_training_dataset(size=ds_size)
+        gts = gts[..., 0]
+    elif data_npz:
         with np.load(data_npz, allow_pickle=False) as z:
             imgs, gts, masks = z["imgs"], z["gts"], z["masks"]
     else:

@@ -88,6 +88,8 @@ _SIGS = {
     "pld_sampler_draw": (I32, [P, I32, I32, I32, U64, U64, I32, P, P]),
     "pld_sampler_rank": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, P, P]),
     "pld_sampler_candidates": (I32, [I32, I32]),
+    "pld_resize_bilinear": (I32, [P, I32, I32, I32, I32, I32, I32, P, P]),
+    "pld_resize_nearest": (I32, [P, I32, I32, I32, I32, I32, I32, P, P]),
     "pld_ordinal_error": (I32, [P, P, I32, I64, P, P, I32, P, P]),
     "pld_dcg_ratio": (I32, [P, P, I32, I64, P, I32, P, P]),
     "pld_graph_begin": (I32, [P]),

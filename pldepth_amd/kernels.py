@@ -539,3 +539,13 @@ def dcg_ratio(pred, gt, ids):
     lib().pld_dcg_ratio(ptr(_f32(pred)), ptr(_f32(gt)), n, hw, ptr(ids), ids.numel(), ptr(out),
                         stream())
     return out
+
+
+# ---- HR-WSI resizing (pld_resize_bilinear / pld_resize_nearest) ----
+def resize(x, oh, ow, method="bilinear", out=None):
+    """x: [n, h, w, c] float32 device tensor -> [n, oh, ow, c] (tf.image.resize, TF2 semantics)."""
+    n, h, w, c = x.shape
+    out = torch.empty((n, oh, ow, c), dtype=torch.float32, device=x.device) if out is None else out
+    fn = lib().pld_resize_bilinear if method == "bilinear" else lib().pld_resize_nearest
+    fn(ptr(_f32(x.contiguous())), n, h, w, c, oh, ow, ptr(out), stream())
+    return out
