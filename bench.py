@@ -70,7 +70,10 @@ def profile_conv(trainer, lr):
             e0.record(st)
             r = fn(args, *rest, **kw)
             e1.record(st)
+            saved = args.tile  # classify by the schedule the call actually ran
+            args.tile = getattr(args, "_used_tile", saved)
             kind = lib().pld_conv_kernel_kind(ctypes.byref(args), mode_of[name])
+            args.tile = saved
             recs.append((kind, flops_of(args), e0, e1))
             return r
         return w

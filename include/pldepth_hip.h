@@ -124,6 +124,13 @@ enum { PLD_MATH_FP32 = 0, PLD_MATH_BF16X3 = 1 };
 int pld_conv_num_tiles(void);
 /* the same for a given PLD_MATH_* */
 int pld_conv_num_schedules(int math);
+/* what schedule `idx` of pld_conv_num_schedules(math) is (for a caller-side tuner): a bf16x3
+ * tile, a bf16x3 tile with split-K, the bf16x3 patch kernel (3x3 convs of 32-channel inputs;
+ * other shapes run the default tile), an fp32 tile, an fp32 tile with split-K; -1 if out of range.
+ * WGRAD sizes its own split: only the tile classes are distinct for it. */
+enum { PLD_SCHED_X3 = 0, PLD_SCHED_X3_SPLIT = 1, PLD_SCHED_X3_PATCH = 2, PLD_SCHED_FP32 = 3,
+       PLD_SCHED_FP32_SPLIT = 4 };
+int pld_conv_schedule_class(int math, int idx);
 /* which kernel family a conv call runs (mode 0 = fwd, 1 = dgrad, 2 = wgrad) for its math and
  * tile: PLD_KIND_FP32 (v_mfma_f32_32x32x2_f32), PLD_KIND_BF16X3 (v_mfma_f32_32x32x16_bf16 x3) or
  * PLD_KIND_DIRECT (single-output-channel VALU kernels); -1 on bad arguments. For roofline

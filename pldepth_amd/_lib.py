@@ -51,6 +51,7 @@ _SIGS = {
     "pld_conv2d_wgrad": (I32, [C.POINTER(ConvArgs), P, P, I32, P, SZ, P]),
     "pld_conv_num_tiles": (I32, []),
     "pld_conv_num_schedules": (I32, [I32]),
+    "pld_conv_schedule_class": (I32, [I32, I32]),
     "pld_conv_kernel_kind": (I32, [C.POINTER(ConvArgs), I32]),
     "pld_conv2d_fwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_dgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
@@ -100,6 +101,7 @@ _SIGS = {
 
 # functions returning a value rather than a status
 _NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_num_schedules",
+               "pld_conv_schedule_class",
                "pld_conv_kernel_kind",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",

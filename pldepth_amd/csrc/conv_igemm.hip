@@ -674,6 +674,9 @@ extern "C" int pld__x3_num_cfg(void);
 extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int* occ);
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
+extern "C" int pld__x3_num_patch(void);
+extern "C" int pld__x3_patch_ok(const GemmConvParams* p);
+extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
 constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
@@ -683,21 +686,31 @@ static bool x3_fwd_geom(int C, int c1, bool prologue, int taps) {
   return C % 8 == 0 && c1 % 8 == 0 && !prologue && taps <= 32;
 }
 
-// Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), then
-// [2 n3, 2 n3 + kNumTiles) the exact-fp32 schedules — the per-shape autotuner may keep fp32
-// where it is faster (e.g. HBM-bound K <= 32 convs); it is never less accurate.
-// Resolves (math, eligible geometry, tile) to (x3 kernel?, tile in that kernel's space).
-static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t) {
-  const int nx = 2 * pld__x3_num_cfg();
+// Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), [2 n3,
+// 2 n3 + np) the bf16x3 patch kernel (3x3, 32-channel inputs; other shapes take the default
+// tile), then [2 n3 + np, ... + kNumTiles) the exact-fp32 schedules — the per-shape autotuner
+// may keep fp32 where it is faster (e.g. HBM-bound K <= 32 convs); it is never less accurate.
+// Resolves (math, eligible geometry, tile) to (x3 kernel?, patch kernel?, tile in that space).
+static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t,
+                          bool* patch = nullptr) {
+  const int n3 = pld__x3_num_cfg(), nx = 2 * n3 + pld__x3_num_patch();
   x3 = false;
   t = tile;
+  if (patch) *patch = false;
   if (math != PLD_MATH_BF16X3) return;
   if (tile >= nx) {
     t = tile - nx;
     return;
   }
-  if (geom_ok) x3 = true;
-  else t = -1;
+  if (!geom_ok) {
+    t = -1;
+    return;
+  }
+  x3 = true;
+  if (tile >= 2 * n3) {
+    t = patch ? tile - 2 * n3 : -1;
+    if (patch) *patch = true;
+  }
 }
 static bool x3_wgrad_geom(int c1, int c2, int cout, bool prologue) {
   return c1 % 16 == 0 && c2 % 16 == 0 && cout % 16 == 0 && !prologue;
@@ -787,8 +800,13 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
                         size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
   bool x3;
+  bool patch;
   resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
-                tile);
+                tile, &patch);
+  if (patch && !pld__x3_patch_ok(&p)) {  // patch schedule on another shape: default tile
+    patch = false;
+    tile = -1;
+  }
   if (x3) {
     PLD_CHECK_ARG(aligned16(p.x1) && (!p.x2 || aligned16(p.x2)) && aligned16(p.bmat) &&
                       (!p.bsplit || aligned16(p.bsplit)),
@@ -803,6 +821,7 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
       if (rc) return rc;
       p.bsplit = wsp;
     }
+    if (patch) return pld__x3_patch_launch(&p, tile, st);
     p.kc_tap = x3_kc_tap(p.kh * p.kw, p.c1, p.c2);
     p.kc1 = (int)cdiv(p.c1, X3_BK);
     x3_fwd_plan(p.M, p.N, p.K, x3_ktiles(p.kc_tap, p.kh * p.kw, p.K), tile, cfg, splits, kt_per);
@@ -911,7 +930,19 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
 extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
 
 extern "C" int pld_conv_num_schedules(int math) {
-  return math == PLD_MATH_BF16X3 ? 2 * pld__x3_num_cfg() + kNumTiles : kNumTiles;
+  return math == PLD_MATH_BF16X3 ? 2 * pld__x3_num_cfg() + pld__x3_num_patch() + kNumTiles
+                                 : kNumTiles;
+}
+
+extern "C" int pld_conv_schedule_class(int math, int idx) {
+  if (idx < 0 || idx >= pld_conv_num_schedules(math)) return -1;
+  const int nf = kNumTiles / 2;  // fp32: [tiles | tiles x split-K]
+  if (math != PLD_MATH_BF16X3) return idx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
+  const int n3 = pld__x3_num_cfg(), nx = 2 * n3 + pld__x3_num_patch();
+  if (idx < n3) return PLD_SCHED_X3;
+  if (idx < 2 * n3) return PLD_SCHED_X3_SPLIT;
+  if (idx < nx) return PLD_SCHED_X3_PATCH;
+  return idx - nx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
 }
 
 extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {

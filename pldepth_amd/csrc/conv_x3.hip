@@ -510,6 +510,156 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvPar
     x3_consumer<BM, BN, WM, WN, MODE>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
 }
 
+// --------------------------------------------------------------------- patch mode
+// 3x3 stride-1 FWD/DGRAD convs whose input has exactly 32 channels (one source): the whole K =
+// 9 taps x 32 channels is ONE input patch. A workgroup stages the 10 x 34-pixel halo patch of an
+// 8 x 32-pixel output tile once (hi/lo planes, [pixel][32 k] rows, chunk_off-swizzled) plus the
+// pre-split filter of its BN output channels for all 9 taps, then each of its 8 waves computes
+// one 32-pixel output row: per tap the A fragments are the patch rows shifted by (ty, tx) —
+// every input value is fetched once per tile instead of once per tap (the im2col GEMM re-reads
+// each input 9 times, which bounds the N <= 96 decoder convs by operand fetch, not MFMA).
+constexpr int PT_H = 8, PT_W = 32, P_H = PT_H + 2, P_W = PT_W + 2, P_PIX = P_H * P_W;
+
+template <int BN>
+struct PatchSmem {
+  static constexpr int A_PLANE = P_PIX * 64;   // [patch pixel][32 k] bf16
+  static constexpr int B_TAP = BN * 64;        // [n][32 k] bf16, one tap
+  static constexpr int B_PLANE = 9 * B_TAP;
+  static constexpr int BYTES = 2 * A_PLANE + 2 * B_PLANE;
+};
+
+template <int BN>
+__global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
+  using S = PatchSmem<BN>;
+  constexpr int TN = BN / 32;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S::BYTES];
+  unsigned char* Ah = smem;
+  unsigned char* Al = smem + S::A_PLANE;
+  unsigned char* Bh = smem + 2 * S::A_PLANE;
+  unsigned char* Bl = Bh + S::B_PLANE;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
+  // XCD-aware order (as conv_x3_kernel): neighbouring tiles, which share halo rows, on one XCD
+  const int nwg = gridDim.x * gridDim.y;
+  const int flat = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xcd = flat & 7, slot = flat >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int nb = wid % gridDim.y;
+  int t = wid / gridDim.y;
+  const int tx0 = t % tiles_x;
+  t /= tiles_x;
+  const int ty0 = t % tiles_y;
+  const int img = t / tiles_y;
+  const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W, n0 = nb * BN;
+
+  // ---- stage: patch (all 512 threads; loads first, then split + stores) ----
+  {
+    const long img_elems = (long)p.h * p.w * 32;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.x1 + img * img_elems, img_elems * 4);
+    constexpr int EA = P_PIX * 8, IA = (EA + 511) / 512;  // 4-channel quads of the patch
+    float4 va[IA];
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int px = e >> 3, q = e & 7;
+      const int py = px / P_W, pxx = px - py * P_W;
+      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+      const bool ok = e < EA && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * 32 + 4 * q) * 4) : OOB);
+    }
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.bsplit, (long)p.N * p.K * 4);
+    constexpr int EB = 9 * BN * 8, IB = (EB + 511) / 512;  // 16-byte halves of 8-k chunks
+    float4 vb[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
+      const int tap = nt / BN, n = nt - tap * BN;
+      const bool ok = e < EB && n0 + n < p.N;
+      vb[i] = bload4(rb, ok ? (unsigned)(((n0 + n) * p.K + tap * 32 + 8 * c) * 4 + 16 * half)
+                            : OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < EA) {
+        const int px = e >> 3, q = e & 7;
+        unsigned h0, l0, h1, l1;
+        split2(va[i].x, va[i].y, h0, l0);
+        split2(va[i].z, va[i].w, h1, l1);
+        const int o = chunk_off(px, q >> 1) + 8 * (q & 1);
+        *reinterpret_cast<u32x2*>(Ah + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(Al + o) = u32x2{l0, l1};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < EB) {
+        const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
+        const int tap = nt / BN, n = nt - tap * BN;
+        *reinterpret_cast<float4*>((half ? Bl : Bh) + tap * S::B_TAP + chunk_off(n, c)) = vb[i];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- compute: wave w = output row oy0 + w, 32 pixels x BN channels ----
+  const int h = lane >> 5, l32 = lane & 31;
+  floatx16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int r = (wave + tap / 3) * P_W + l32 + tap % 3;  // this lane's patch pixel
+    const unsigned char* bh_t = Bh + tap * S::B_TAP;
+    const unsigned char* bl_t = Bl + tap * S::B_TAP;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 ah = lds_frag(Ah, r, 2 * s + h), al = lds_frag(Al, r, 2 * s + h);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const bf16x8 bh = lds_frag(bh_t, b * 32 + l32, 2 * s + h);
+        const bf16x8 bl = lds_frag(bl_t, b * 32 + l32, 2 * s + h);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[b], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: tile row i = output pixel ox0 + i of row oy0 + wave (bias, routing, acc) ----
+  const int oy = oy0 + wave;
+  if (oy >= p.oh) return;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n0 + b * 32 + l32;
+    if (col >= p.N) continue;
+    const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ox = ox0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ox >= p.ow) continue;
+      const long row = ((long)img * p.oh + oy) * p.ow + ox;
+      const float v = acc[b][r] + bias;
+      if (col < p.split) {
+        float* dst = p.out1 + row * p.ld1 + col;
+        *dst = p.acc1 ? *dst + v : v;
+      } else {
+        float* dst = p.out2 + row * p.ld2 + (col - p.split);
+        *dst = p.acc2 ? *dst + v : v;
+      }
+    }
+  }
+}
+
+constexpr int kPatchBN[] = {32, 64, 96};
+constexpr int kNumPatch = 3;
+
 // ------------------------------------------------------------------------ schedules
 struct Cfg { int bm, bn, tm, tn, occ; };
 // occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
@@ -590,6 +740,32 @@ extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int
 }
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg) {  // every tile (widths 32..256, % 32)
   return cfg >= 0 && cfg < x3::kNumCfg;
+}
+extern "C" int pld__x3_num_patch(void) { return x3::kNumPatch; }
+extern "C" int pld__x3_patch_bn(int cfg) {
+  return cfg >= 0 && cfg < x3::kNumPatch ? x3::kPatchBN[cfg] : 0;
+}
+// eligibility of the patch kernel (FWD view): 3x3 stride 1, one 32-channel source, no prologue
+extern "C" int pld__x3_patch_ok(const GemmConvParams* p) {
+  return p->C == 32 && p->c2 == 0 && p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 &&
+         p->in_scale == nullptr && p->K == 288 && p->pt >= 0 && p->pt <= 2 && p->pl >= 0 &&
+         p->pl <= 2;
+}
+extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream) {
+  if (!pld__x3_patch_ok(p) || cfg < 0 || cfg >= x3::kNumPatch || !p->bsplit) {
+    set_error("conv_x3_patch: ineligible geometry or schedule %d", cfg);
+    return PLD_ERR_ARG;
+  }
+  const int tiles = (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, x3::PT_H) * p->n);
+  const int bn = x3::kPatchBN[cfg];
+  dim3 grid(tiles, cdiv(p->N, bn));
+  hipStream_t st = as_stream(stream);
+  switch (cfg) {
+    case 0: x3::conv_x3_patch_kernel<32><<<grid, 512, 0, st>>>(*p); break;
+    case 1: x3::conv_x3_patch_kernel<64><<<grid, 512, 0, st>>>(*p); break;
+    default: x3::conv_x3_patch_kernel<96><<<grid, 512, 0, st>>>(*p); break;
+  }
+  return check_launch("conv_x3_patch_kernel");
 }
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {

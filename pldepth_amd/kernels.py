@@ -117,11 +117,8 @@ def same_pads(h, k, s):
 
 
 # conv product arithmetic (pld_conv_args.math): "bf16x3" (fp32 via three bf16 MFMA products,
-# ~1e-5 relative per product) or "fp32" (exact fp32 MFMA). The model engines apply a policy:
-# "mixed" (default) runs the encoder's convs in fp32 and the decoder's in bf16x3 — the deep
-# training-mode-BN encoder chain amplifies per-op rounding at small batch sizes, while the decoder
-# holds ~83 % of the conv FLOPs; "bf16x3" / "fp32" use one arithmetic everywhere.
-# PLD_CONV_MATH overrides the default policy.
+# ~1e-5 relative per product) or "fp32" (exact fp32 MFMA). The model engines apply a policy
+# (below); PLD_CONV_MATH overrides the default one.
 MATH = {"fp32": 0, "bf16x3": 1}
 # conv arithmetic policies: "auto" (default) = decoder bf16x3, encoder bf16x3
 # where the BN after the conv normalises over >= X3_MIN_POPULATION values per channel, exact
@@ -226,18 +223,27 @@ def _skinny(a):
             and not a.in_scale and a.c1 % 4 == 0 and a.c1 <= 64)
 
 
-def _schedules(mode, math):
-    """Schedule indices worth timing (pld_conv_args.tile). fwd/dgrad: every tile x split-K
-    schedule; wgrad always sizes its own split, so only the tiles. Under bf16x3 the exact-fp32
-    schedules follow the bf16x3 ones."""
-    nf = lib().pld_conv_num_tiles()
+def _patch_ok(mode, a):
+    """Shapes the bf16x3 patch kernel takes (pld__x3_patch_ok, FWD view of fwd / dgrad)."""
+    if mode == "wgrad" or a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1 or a.in_scale:
+        return False
+    return (a.c1 == 32 and a.c2 == 0) if mode == "fwd" else a.cout == 32
+
+
+def _schedules(mode, math, a=None):
+    """Schedule indices worth timing (pld_conv_args.tile): fwd/dgrad every tile x split-K
+    schedule (+ the patch kernel where it applies); wgrad sizes its own split, so only the tiles.
+    Under bf16x3 the exact-fp32 schedules follow the bf16x3 ones."""
     n = lib().pld_conv_num_schedules(math)
-    if mode != "wgrad":
-        return list(range(n))
-    if n == nf:
-        return list(range(nf // 2))
-    nx = n - nf
-    return list(range(nx // 2)) + list(range(nx, nx + nf // 2))
+    out = []
+    for i in range(n):
+        c = lib().pld_conv_schedule_class(math, i)
+        if mode == "wgrad" and c not in (0, 3):
+            continue
+        if c == 2 and (a is None or not _patch_ok(mode, a)):
+            continue
+        out.append(i)
+    return out
 
 
 def _tune(mode, a, run):
@@ -250,7 +256,7 @@ def _tune(mode, a, run):
         return -1
     best, best_t = -1, float("inf")
     st = torch.cuda.current_stream()
-    for t in _schedules(mode, a.math):
+    for t in _schedules(mode, a.math, a):
         run(t)  # warm-up (also sizes the workspace)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
@@ -291,7 +297,20 @@ def _set_split(args, w):
     args.w_split = None if s is None else s.data_ptr()
 
 
+def _begin(args):
+    """The caller's schedule request (-1 = tune per shape). One args object may serve the fwd,
+    dgrad and wgrad of a conv: the schedule each call resolves is recorded in args._used_tile and
+    args.tile is restored afterwards (_end), so a wgrad-tuned tile never leaks into the dgrad."""
+    return args.tile
+
+
+def _end(args, tile_in):
+    args._used_tile = args.tile
+    args.tile = tile_in
+
+
 def conv2d_fwd(args, w_native, bias, y, accumulate=False):
+    tile_in = _begin(args)
     _set_split(args, w_native)
     if args.tile < 0:
         scratch = None
@@ -307,10 +326,12 @@ def conv2d_fwd(args, w_native, bias, y, accumulate=False):
     _splitk_ws(args, lib().pld_conv2d_fwd_workspace_size)
     lib().pld_conv2d_fwd(C.byref(args), ptr(w_native), ptr(bias), ptr(y), int(accumulate),
                          stream())
+    _end(args, tile_in)
     return y
 
 
 def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
+    tile_in = _begin(args)
     _set_split(args, w_dgrad)
     if args.tile < 0:
         s1 = s2 = None
@@ -327,9 +348,11 @@ def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
     _splitk_ws(args, lib().pld_conv2d_dgrad_workspace_size)
     lib().pld_conv2d_dgrad(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(dx1), int(acc1), ptr(dx2),
                            int(acc2), stream())
+    _end(args, tile_in)
 
 
 def conv2d_wgrad(args, dy, dw, accumulate=False):
+    tile_in = _begin(args)
     if args.tile < 0:
         sdw = None
 
@@ -345,6 +368,7 @@ def conv2d_wgrad(args, dy, dw, accumulate=False):
     ws = workspace(need, "wgrad") if need else None
     lib().pld_conv2d_wgrad(C.byref(args), ptr(dy), ptr(dw), int(accumulate), ptr(ws), need,
                            stream())
+    _end(args, tile_in)
 
 
 def channel_sum(x, rows, c, out, accumulate=False):
