@@ -677,6 +677,8 @@ extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, 
 extern "C" int pld__x3_num_patch(void);
 extern "C" int pld__x3_patch_ok(const GemmConvParams* p);
 extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
+extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
+extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream);
 constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
@@ -1086,14 +1088,37 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
                       "pld_conv2d_dgrad", a->math);
 }
 
+// the bf16x3 patch WGRAD kernel's geometry (pld__x3_patch_wgrad_ok, from the call's args)
+static bool wgrad_patch_geom(const pld_conv_args* a) {
+  return a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 && a->in_scale == nullptr &&
+         a->c1 % 16 == 0 && a->c2 % 16 == 0 && a->cout % 4 == 0 && a->pad_t >= 0 &&
+         a->pad_t <= 2 && a->pad_l >= 0 && a->pad_l <= 2;
+}
+
 static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& splits,
-                       int& kt_per, int& cfg, bool& x3) {
+                       int& kt_per, int& cfg, bool& x3, bool* patch_out = nullptr) {
   M = a->kh * a->kw * (a->c1 + a->c2);
   N = a->cout;
   K = (long)a->n * a->oh * a->ow;
   int tile;
+  bool patch;
   resolve_sched(a->math, x3_wgrad_geom(a->c1, a->c2, a->cout, a->in_scale != nullptr), a->tile,
-                x3, tile);
+                x3, tile, &patch);
+  if (patch && !wgrad_patch_geom(a)) {
+    patch = false;
+    tile = -1;
+  }
+  if (patch_out) *patch_out = patch;
+  if (patch) {  // patch schedule: workgroups = chunks x 32-cout tiles x splits, ~512 in all
+    const long tiles = (long)cdiv(a->ow, 32) * cdiv(a->oh, 8) * a->n;
+    const long blocks = (long)(cdiv(a->c1, 32) + cdiv(a->c2, 32)) * cdiv(N, 32);
+    long s = std::max<long>(1, (512 + blocks - 1) / blocks);
+    s = std::min<long>(s, tiles);
+    kt_per = (int)((tiles + s - 1) / s);
+    splits = (int)((tiles + kt_per - 1) / kt_per);
+    cfg = 0;
+    return;
+  }
   const int bk = x3 ? X3_BK : BK;
   const long ktiles = (K + bk - 1) / bk;
   // pick the tile for an unsplit GEMM, then split K until ~2-3 blocks per CU
@@ -1157,8 +1182,8 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   }
   int M, N, splits, kt_per, cfg;
   long K;
-  bool x3;
-  wgrad_plan(a, M, N, K, splits, kt_per, cfg, x3);
+  bool x3, patch;
+  wgrad_plan(a, M, N, K, splits, kt_per, cfg, x3, &patch);
   PLD_CHECK_ARG(K < (1L << 31), "pld_conv2d_wgrad: too many pixels");
   const size_t need = wgrad_ws_bytes(splits, M, N);
   PLD_CHECK_ARG(ws_bytes >= need && (need == 0 || ws),
@@ -1185,7 +1210,13 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   const bool vec = (p.c1 % 4 == 0) && (p.c2 % 4 == 0) && aligned16(p.x1) &&
                    (!p.x2 || aligned16(p.x2)) && aligned16(dy) &&
                    (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift)));
-  if (x3) {
+  if (patch) {
+    PLD_CHECK_ARG(vec, "pld_conv2d_wgrad: bf16x3 operands must be 16-byte aligned");
+    PLD_CHECK_ARG((long)a->h * a->w * std::max(a->c1, a->c2) * 4 < MAX_RECORDS &&
+                      (long)a->oh * a->ow * N * 4 < MAX_RECORDS,
+                  "pld_conv2d_wgrad: image too large for 32-bit buffer offsets");
+    rc = pld__x3_patch_wgrad_launch(&p, splits, st);
+  } else if (x3) {
     PLD_CHECK_ARG(vec, "pld_conv2d_wgrad: bf16x3 operands must be 16-byte aligned");
     rc = pld__x3_launch(&p, MODE_WGRAD, splits, cfg, st);
   } else {

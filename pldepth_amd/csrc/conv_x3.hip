@@ -660,6 +660,171 @@ __global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
 constexpr int kPatchBN[] = {32, 64, 96};
 constexpr int kNumPatch = 3;
 
+// WGRAD in patch form, 3x3 stride 1: dW[tap][ci][co] = sum_p X[p + tap][ci] dY[p][co]. A
+// workgroup owns one 32-channel chunk of ONE source (all 9 taps: 9 MFMA row tiles) x 32 output
+// channels, and loops over a range of 8 x 32-pixel output tiles (its split-K share). Per tile it
+// stages the 10 x 34 input patch of the chunk and the 256 x 32 dY tile as [pixel][channel] hi/lo
+// images, double-buffered; each of the 8 waves takes one output row (two 16-pixel k-steps) and
+// accumulates all 9 taps — the A fragment of tap (ty, tx) is the patch image read transposed
+// (ds_read_b64_tr_b16) from row (row + ty) * 34 + tx on, the dY fragment is shared by the 9
+// taps. Every input value is staged once per tile, not once per tap. The 8 waves' partial sums
+// are combined in LDS by a fixed tree at the end (deterministic).
+constexpr int PW_A = P_PIX * 64;       // patch image plane: [340 pixels][32 ch] bf16
+constexpr int PW_B = PT_H * PT_W * 64; // dY image plane: [256 pixels][32 co] bf16
+constexpr int PW_STAGE = 2 * PW_A + 2 * PW_B;
+
+__device__ __forceinline__ bf16x8 tr_frag_rows(const unsigned char* plane, int row0, int lane) {
+  // 32x32x16 operand from a [row][32 col] bf16 image (64-byte rows, no swizzle: 4 consecutive
+  // rows land 16 banks apart): lane l needs column l & 31 and rows row0 + 8 (l >> 5) .. +7
+  const int i16 = lane & 15, grp = (lane >> 4) & 1, h = lane >> 5;
+  const int r = row0 + 8 * h + (i16 >> 2);
+  const int col = 16 * grp + 4 * (i16 & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + r * 64 + col * 2));
+  const v4s hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + (r + 4) * 64 + col * 2));
+  const v4s v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(512) void conv_x3_patch_wgrad_kernel(GemmConvParams p, int tiles,
+                                                                  int tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PW_STAGE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  const bool s2 = q >= p.kc1;
+  const int cb = (s2 ? q - p.kc1 : q) * 32;  // first channel of the chunk in its source
+  const int cs = s2 ? p.c2 : p.c1;
+  const int nv = min(32, cs - cb);           // valid channels of the chunk
+  const int n0 = nb * 32;
+  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
+  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
+  const long img_in = (long)p.h * p.w * cs;
+  const float* xsrc = s2 ? p.x2 : p.x1;
+
+  constexpr int EA = P_PIX * 8, IA = (EA + 511) / 512;  // patch: 4-channel quads
+  constexpr int EB = PT_H * PT_W * 8, IB = EB / 512;    // dY: 4-channel quads
+  float4 va[IA], vb[IB];
+  auto load = [&](int t) {
+    t = min(t, t_end - 1);  // past the end: a harmless re-load of the last tile
+    const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
+    const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int px = e >> 3, c4 = (e & 7) * 4;
+      const int py = px / P_W, pxx = px - py * P_W;
+      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+      const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
+                      (unsigned)ix < (unsigned)p.w;
+      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
+    }
+    const long img_out = (long)p.oh * p.ow;
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int k = e >> 3, c4 = (e & 7) * 4;
+      const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
+      const bool ok = oy < p.oh && ox < p.ow && n0 + c4 < p.N;
+      vb[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned char* A = smem + buf * PW_STAGE;
+    unsigned char* B = A + 2 * PW_A;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < EA) {
+        unsigned h0, l0, h1, l1;
+        split2(va[i].x, va[i].y, h0, l0);
+        split2(va[i].z, va[i].w, h1, l1);
+        const int o = (e >> 3) * 64 + (e & 7) * 8;
+        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(A + PW_A + o) = u32x2{l0, l1};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      unsigned h0, l0, h1, l1;
+      split2(vb[i].x, vb[i].y, h0, l0);
+      split2(vb[i].z, vb[i].w, h1, l1);
+      const int o = (e >> 3) * 64 + (e & 7) * 8;
+      *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(B + PW_B + o) = u32x2{l0, l1};
+    }
+  };
+
+  floatx16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  if (t_begin < t_end) {
+    load(t_begin);
+    store(0);
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      const int buf = (t - t_begin) & 1;
+      load(t + 1);
+      const unsigned char* A = smem + buf * PW_STAGE;
+      const unsigned char* B = A + 2 * PW_A;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int k0 = 32 * wave + 16 * s;  // this wave's 16 output pixels (row `wave`)
+        const bf16x8 bh = tr_frag_rows(B, k0, lane), bl = tr_frag_rows(B + PW_B, k0, lane);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int r0 = (wave + tap / 3) * P_W + 16 * s + tap % 3;
+          const bf16x8 ah = tr_frag_rows(A, r0, lane), al = tr_frag_rows(A + PW_A, r0, lane);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
+        }
+      }
+      if (t + 1 < t_end) store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // combine the 8 waves: 4 -> 0..3, 2 -> 0..1, 1 -> 0 through LDS (fixed tree)
+  float* red = reinterpret_cast<float*>(smem);  // 4 slots x 9 tiles x 64 lanes x 16
+  for (int half = 4; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+      float* slot = red + (long)(wave - half) * 9 * 64 * 16;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) slot[(t * 16 + r) * 64 + lane] = acc[t][r];
+    }
+    __syncthreads();
+    if (wave < half) {
+      const float* slot = red + (long)wave * 9 * 64 * 16;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] += slot[(t * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  if (wave != 0) return;
+  const int h = lane >> 5, col = n0 + (lane & 31);
+  if (col >= p.N) return;
+  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ci >= nv) continue;
+      const long m = (long)t * p.C + (s2 ? p.c1 : 0) + cb + ci;
+      float* dst = out + m * p.N + col;
+      *dst = (p.zstride == 0 && p.acc1) ? *dst + acc[t][r] : acc[t][r];
+    }
+}
+
 // ------------------------------------------------------------------------ schedules
 struct Cfg { int bm, bn, tm, tn, occ; };
 // occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
@@ -766,6 +931,29 @@ extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream) {
     default: x3::conv_x3_patch_kernel<96><<<grid, 512, 0, st>>>(*p); break;
   }
   return check_launch("conv_x3_patch_kernel");
+}
+// WGRAD patch kernel: 3x3 stride 1, channel counts that split into 32-channel chunks of one
+// source (c1, c2 % 16 == 0), no prologue; `splits` workgroups per (chunk, 32 cout) share the tiles
+extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p) {
+  return p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 && p->in_scale == nullptr &&
+         p->c1 % 16 == 0 && p->c2 % 16 == 0 && p->N % 4 == 0 && p->pt >= 0 && p->pt <= 2 &&
+         p->pl >= 0 && p->pl <= 2;
+}
+extern "C" int pld__x3_patch_wgrad_tiles(const GemmConvParams* p) {
+  return (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, x3::PT_H) * p->n);
+}
+extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream) {
+  if (!pld__x3_patch_wgrad_ok(p) || splits < 1) {
+    set_error("conv_x3_patch_wgrad: ineligible geometry");
+    return PLD_ERR_ARG;
+  }
+  const int tiles = pld__x3_patch_wgrad_tiles(p);
+  const int tps = (int)cdiv(tiles, splits);
+  p->kc1 = (int)cdiv(p->c1, 32);
+  const int chunks = p->kc1 + (int)cdiv(p->c2, 32);
+  dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
+  x3::conv_x3_patch_wgrad_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
+  return check_launch("conv_x3_patch_wgrad_kernel");
 }
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {

@@ -224,9 +224,12 @@ def _skinny(a):
 
 
 def _patch_ok(mode, a):
-    """Shapes the bf16x3 patch kernel takes (pld__x3_patch_ok, FWD view of fwd / dgrad)."""
-    if mode == "wgrad" or a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1 or a.in_scale:
+    """Shapes the bf16x3 patch kernels take (pld__x3_patch_ok for the FWD view of fwd / dgrad;
+    pld__x3_patch_wgrad_ok for wgrad)."""
+    if a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1 or a.in_scale:
         return False
+    if mode == "wgrad":
+        return a.c1 % 16 == 0 and a.c2 % 16 == 0 and a.cout % 4 == 0
     return (a.c1 == 32 and a.c2 == 0) if mode == "fwd" else a.cout == 32
 
 
@@ -235,10 +238,14 @@ def _schedules(mode, math, a=None):
     schedule (+ the patch kernel where it applies); wgrad sizes its own split, so only the tiles.
     Under bf16x3 the exact-fp32 schedules follow the bf16x3 ones."""
     n = lib().pld_conv_num_schedules(math)
-    out = []
+    out, patch_seen = [], False
     for i in range(n):
         c = lib().pld_conv_schedule_class(math, i)
-        if mode == "wgrad" and c not in (0, 3):
+        if c == 2 and mode == "wgrad":  # one wgrad patch schedule (it sizes its own split)
+            if patch_seen:
+                continue
+            patch_seen = True
+        if mode == "wgrad" and c not in (0, 2, 3):
             continue
         if c == 2 and (a is None or not _patch_ok(mode, a)):
             continue
