@@ -675,7 +675,7 @@ extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
 extern "C" int pld__x3_num_patch(void);
-extern "C" int pld__x3_patch_ok(const GemmConvParams* p);
+extern "C" int pld__x3_patch_ok(const GemmConvParams* p, int cfg);
 extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
 extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream);
@@ -805,7 +805,7 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   bool patch;
   resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
                 tile, &patch);
-  if (patch && !pld__x3_patch_ok(&p)) {  // patch schedule on another shape: default tile
+  if (patch && !pld__x3_patch_ok(&p, tile)) {  // patch schedule on another shape: default tile
     patch = false;
     tile = -1;
   }

@@ -657,6 +657,146 @@ __global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
   }
 }
 
+// The same for inputs of several 32-channel chunks (C % 16 == 0 per source; a concat's sources
+// chunked separately, a ragged 16-channel chunk masked): 32 output channels per workgroup, the
+// (patch, filter) stage of chunk i+1 loaded into registers while chunk i is multiplied, double
+// buffered in LDS (2 x 80 KB).
+constexpr int MC_STAGE = 2 * PatchSmem<32>::A_PLANE + 2 * PatchSmem<32>::B_PLANE;
+
+template <bool CAT>
+__global__ __launch_bounds__(512) void conv_x3_patch_mc_kernel(GemmConvParams p) {
+  using S = PatchSmem<32>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * MC_STAGE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
+  const int nwg = gridDim.x * gridDim.y;
+  const int flat = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xcd = flat & 7, slot = flat >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int nb = wid % gridDim.y;
+  int t = wid / gridDim.y;
+  const int tx0 = t % tiles_x;
+  t /= tiles_x;
+  const int ty0 = t % tiles_y;
+  const int img = t / tiles_y;
+  const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W, n0 = nb * 32;
+  const int nch = p.kc_tap;  // chunks: kc1 of x1, then those of x2
+  const long img1 = (long)p.h * p.w * p.c1, img2 = (long)p.h * p.w * p.c2;
+  const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.x1 + img * img1, img1 * 4);
+  const __amdgpu_buffer_rsrc_t rs2 = CAT ? make_rsrc(p.x2 + img * img2, img2 * 4) : rs1;
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.bsplit, (long)p.N * p.K * 4);
+
+  constexpr int EA = P_PIX * 8, IA = (EA + 511) / 512;
+  constexpr int EB = 9 * 32 * 8, IB = (EB + 511) / 512;
+  float4 va[IA], vb[IB];
+  auto load = [&](int ch) {
+    ch = min(ch, nch - 1);
+    const bool s2 = CAT && ch >= p.kc1;
+    const int cb = (s2 ? ch - p.kc1 : ch) * 32, cs = s2 ? p.c2 : p.c1;
+    const __amdgpu_buffer_rsrc_t rs = s2 ? rs2 : rs1;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int px = e >> 3, c4 = (e & 7) * 4;
+      const int py = px / P_W, pxx = px - py * P_W;
+      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+      const bool ok = e < EA && cb + c4 < cs && (unsigned)iy < (unsigned)p.h &&
+                      (unsigned)ix < (unsigned)p.w;
+      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
+    }
+    const int kb = (s2 ? p.c1 : 0) + cb;  // chunk's first channel in the filter's k = tap C + ci
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
+      const int tap = nt >> 5, n = nt & 31;
+      const bool ok = e < EB && n0 + n < p.N && cb + 8 * c < cs;
+      vb[i] = bload4(rb, ok ? (unsigned)(((n0 + n) * p.K + tap * p.C + kb + 8 * c) * 4 + 16 * half)
+                            : OOB);
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned char* Ah = smem + buf * MC_STAGE;
+    unsigned char* Al = Ah + S::A_PLANE;
+    unsigned char* Bh = Ah + 2 * S::A_PLANE;
+    unsigned char* Bl = Bh + S::B_PLANE;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < EA) {
+        const int px = e >> 3, q = e & 7;
+        unsigned h0, l0, h1, l1;
+        split2(va[i].x, va[i].y, h0, l0);
+        split2(va[i].z, va[i].w, h1, l1);
+        const int o = chunk_off(px, q >> 1) + 8 * (q & 1);
+        *reinterpret_cast<u32x2*>(Ah + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(Al + o) = u32x2{l0, l1};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < EB) {
+        const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
+        const int tap = nt >> 5, n = nt & 31;
+        *reinterpret_cast<float4*>((half ? Bl : Bh) + tap * S::B_TAP + chunk_off(n, c)) = vb[i];
+      }
+    }
+  };
+
+  const int h = lane >> 5, l32 = lane & 31;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    load(ch + 1);
+    const unsigned char* Ah = smem + buf * MC_STAGE;
+    const unsigned char* Al = Ah + S::A_PLANE;
+    const unsigned char* Bh = Ah + 2 * S::A_PLANE;
+    const unsigned char* Bl = Bh + S::B_PLANE;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = (wave + tap / 3) * P_W + l32 + tap % 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 ah = lds_frag(Ah, r, 2 * s + h), al = lds_frag(Al, r, 2 * s + h);
+        const bf16x8 bh = lds_frag(Bh + tap * S::B_TAP, l32, 2 * s + h);
+        const bf16x8 bl = lds_frag(Bl + tap * S::B_TAP, l32, 2 * s + h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  const int oy = oy0 + wave;
+  const int col = n0 + l32;
+  if (oy >= p.oh || col >= p.N) return;
+  const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ox = ox0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (ox >= p.ow) continue;
+    const long row = ((long)img * p.oh + oy) * p.ow + ox;
+    const float v = acc[r] + bias;
+    if (col < p.split) {
+      float* dst = p.out1 + row * p.ld1 + col;
+      *dst = p.acc1 ? *dst + v : v;
+    } else {
+      float* dst = p.out2 + row * p.ld2 + (col - p.split);
+      *dst = p.acc2 ? *dst + v : v;
+    }
+  }
+}
+
 constexpr int kPatchBN[] = {32, 64, 96};
 constexpr int kNumPatch = 3;
 
@@ -910,18 +1050,30 @@ extern "C" int pld__x3_num_patch(void) { return x3::kNumPatch; }
 extern "C" int pld__x3_patch_bn(int cfg) {
   return cfg >= 0 && cfg < x3::kNumPatch ? x3::kPatchBN[cfg] : 0;
 }
-// eligibility of the patch kernel (FWD view): 3x3 stride 1, one 32-channel source, no prologue
-extern "C" int pld__x3_patch_ok(const GemmConvParams* p) {
-  return p->C == 32 && p->c2 == 0 && p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 &&
-         p->in_scale == nullptr && p->K == 288 && p->pt >= 0 && p->pt <= 2 && p->pl >= 0 &&
-         p->pl <= 2;
+// eligibility of the patch kernels (FWD view): 3x3 stride 1, no prologue; one 32-channel source
+// for every schedule, or channels in 16s per source for the multi-chunk (32-column) schedule 0
+extern "C" int pld__x3_patch_ok(const GemmConvParams* p, int cfg) {
+  const bool geo = p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 &&
+                   p->in_scale == nullptr && p->K == 9 * p->C && p->pt >= 0 && p->pt <= 2 &&
+                   p->pl >= 0 && p->pl <= 2;
+  if (!geo) return 0;
+  if (p->C == 32 && p->c2 == 0) return 1;
+  return cfg == 0 && p->c1 % 16 == 0 && p->c2 % 16 == 0;
 }
 extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream) {
-  if (!pld__x3_patch_ok(p) || cfg < 0 || cfg >= x3::kNumPatch || !p->bsplit) {
+  if (!pld__x3_patch_ok(p, cfg) || cfg < 0 || cfg >= x3::kNumPatch || !p->bsplit) {
     set_error("conv_x3_patch: ineligible geometry or schedule %d", cfg);
     return PLD_ERR_ARG;
   }
   const int tiles = (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, x3::PT_H) * p->n);
+  if (!(p->C == 32 && p->c2 == 0)) {  // multi-chunk
+    p->kc1 = (int)cdiv(p->c1, 32);
+    p->kc_tap = p->kc1 + (int)cdiv(p->c2, 32);
+    dim3 grid(tiles, cdiv(p->N, 32));
+    if (p->c2) x3::conv_x3_patch_mc_kernel<true><<<grid, 512, 0, as_stream(stream)>>>(*p);
+    else x3::conv_x3_patch_mc_kernel<false><<<grid, 512, 0, as_stream(stream)>>>(*p);
+    return check_launch("conv_x3_patch_mc_kernel");
+  }
   const int bn = x3::kPatchBN[cfg];
   dim3 grid(tiles, cdiv(p->N, bn));
   hipStream_t st = as_stream(stream);

@@ -230,7 +230,9 @@ def _patch_ok(mode, a):
         return False
     if mode == "wgrad":
         return a.c1 % 16 == 0 and a.c2 % 16 == 0 and a.cout % 4 == 0
-    return (a.c1 == 32 and a.c2 == 0) if mode == "fwd" else a.cout == 32
+    # fwd / dgrad (FWD view: dgrad's input is dY): one 32-channel source for all three patch
+    # schedules, channels in 16s per source for the multi-chunk one
+    return (a.c1 % 16 == 0 and a.c2 % 16 == 0) if mode == "fwd" else a.cout % 16 == 0
 
 
 def _schedules(mode, math, a=None):
