@@ -287,6 +287,16 @@ int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const float* w1, c
 int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c, int cse, const float* w1,
                const float* w2, const float* z1, const float* gate, float* addn, void* ws,
                void* stream);
+/* the same with a = act(((x - mean) * invstd) * gamma + beta) computed on the fly from the
+ * block's pre-BN depthwise output x (the activation need not be materialised in training) */
+int pld_se_fwd_bn(const float* x, const float* mean, const float* invstd, const float* gamma,
+                  const float* beta, int act, int n, int hw, int c, int cse, const float* w1,
+                  const float* b1, const float* w2, const float* b2, float* pooled, float* z1,
+                  float* gate, void* ws, void* stream);
+int pld_se_bwd_bn(const float* dy, const float* x, const float* mean, const float* invstd,
+                  const float* gamma, const float* beta, int act, int n, int hw, int c, int cse,
+                  const float* w1, const float* w2, const float* z1, const float* gate,
+                  float* addn, void* ws, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Ranking sampler (pldepth/data/sampling.py), split into draws and a deterministic part.

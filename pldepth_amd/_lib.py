@@ -83,6 +83,8 @@ _SIGS = {
     "pld_se_workspace_size": (SZ, [I32, I32, I32, I32]),
     "pld_se_fwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
     "pld_se_bwd": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P]),
+    "pld_se_fwd_bn": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
+    "pld_se_bwd_bn": (I32, [P, P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, P]),
     "pld_sampler_workspace_size": (SZ, [I32, I32, I32, I32, I32, I32]),
     "pld_sampler_compact": (I32, [P, I32, I32, I32, P, P, P, P, P, P]),
     "pld_sampler_compact_workspace_size": (SZ, [I32, I32, I32]),

@@ -239,10 +239,30 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restri
 }
 
 // ---- SE ----
-// per-image channel sums of a (or of a*dy): partial[img][split][c] (fp64)
+// optional input prologue of the SE reductions: the squeeze reads the pre-BN depthwise output
+// and applies the block's BN + activation on the fly, so the activation is never materialised
+struct SePro {
+  const float* mean;  // NULL: the input is already the activation
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+};
+
+__device__ __forceinline__ float4 se_pro(const SePro& pr, float4 v, float4 mu, float4 is,
+                                         float4 ga, float4 be) {
+  return make_float4(act_fwd(pr.act, ((v.x - mu.x) * is.x) * ga.x + be.x),
+                     act_fwd(pr.act, ((v.y - mu.y) * is.y) * ga.y + be.y),
+                     act_fwd(pr.act, ((v.z - mu.z) * is.z) * ga.z + be.z),
+                     act_fwd(pr.act, ((v.w - mu.w) * is.w) * ga.w + be.w));
+}
+
+// per-image channel sums of a (or of a*dy): partial[img][split][c] (fp64); 4 rows of loads in
+// flight per thread (the same summation order as one row at a time)
+template <bool PRO>
 __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restrict__ a,
                                                            const float* __restrict__ b, int hw,
-                                                           int c, int rsplit,
+                                                           int c, int rsplit, SePro pr,
                                                            double* __restrict__ part) {
   const int img = blockIdx.x / rsplit;
   const int sp = blockIdx.x % rsplit;
@@ -258,15 +278,49 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
   double s[4] = {0.0, 0.0, 0.0, 0.0};
   if (r0 < rpi) {
     const long base = (long)img * hw * c + 4 * q;
-    for (int r = rb + r0; r < re; r += rpi) {
-      const float4 v = *reinterpret_cast<const float4*>(a + base + (long)r * c);
+    float4 mu, is, ga, be;
+    if (PRO) {
+      mu = *reinterpret_cast<const float4*>(pr.mean + 4 * q);
+      is = *reinterpret_cast<const float4*>(pr.invstd + 4 * q);
+      ga = *reinterpret_cast<const float4*>(pr.gamma + 4 * q);
+      be = *reinterpret_cast<const float4*>(pr.beta + 4 * q);
+    }
+    auto acc1 = [&](float4 v, float4 u) {
+      if (PRO) v = se_pro(pr, v, mu, is, ga, be);
       if (b) {
-        const float4 u = *reinterpret_cast<const float4*>(b + base + (long)r * c);
         s[0] += (double)(v.x * u.x); s[1] += (double)(v.y * u.y);
         s[2] += (double)(v.z * u.z); s[3] += (double)(v.w * u.w);
       } else {
         s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
       }
+    };
+    int r = rb + r0;
+    constexpr int RU = 4;
+    if (b) {
+      for (; r + (RU - 1) * rpi < re; r += RU * rpi) {
+        float4 v[RU], u[RU];
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+          v[j] = *reinterpret_cast<const float4*>(a + base + (long)(r + j * rpi) * c);
+          u[j] = *reinterpret_cast<const float4*>(b + base + (long)(r + j * rpi) * c);
+        }
+#pragma unroll
+        for (int j = 0; j < RU; ++j) acc1(v[j], u[j]);
+      }
+    } else {
+      for (; r + (RU - 1) * rpi < re; r += RU * rpi) {
+        float4 v[RU];
+#pragma unroll
+        for (int j = 0; j < RU; ++j)
+          v[j] = *reinterpret_cast<const float4*>(a + base + (long)(r + j * rpi) * c);
+#pragma unroll
+        for (int j = 0; j < RU; ++j) acc1(v[j], v[j]);
+      }
+    }
+    for (; r < re; r += rpi) {
+      const float4 v = *reinterpret_cast<const float4*>(a + base + (long)r * c);
+      const float4 u = b ? *reinterpret_cast<const float4*>(b + base + (long)r * c) : v;
+      acc1(v, u);
     }
   }
   __shared__ double red[256][4];
@@ -511,9 +565,9 @@ extern "C" size_t pld_se_workspace_size(int n, int hw, int c, int cse) {
   return sizeof(double) * (size_t)n * se_rsplit(n, hw, c) * c;
 }
 
-extern "C" int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const float* w1,
-                          const float* b1, const float* w2, const float* b2, float* pooled,
-                          float* z1, float* gate, void* ws, void* stream) {
+static int se_fwd_impl(const float* a, const SePro& pr, int n, int hw, int c, int cse,
+                       const float* w1, const float* b1, const float* w2, const float* b2,
+                       float* pooled, float* z1, float* gate, void* ws, void* stream) {
   PLD_CHECK_ARG(a && w1 && b1 && w2 && b2 && pooled && z1 && gate && ws && n > 0 && hw > 0 &&
                     c > 0 && cse > 0,
                 "pld_se_fwd: bad args");
@@ -521,7 +575,8 @@ extern "C" int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const f
   hipStream_t st = as_stream(stream);
   const int rs = se_rsplit(n, hw, c);
   dim3 g1(n * rs, cdiv(c / 4, 256));
-  img_chan_sum_kernel<<<g1, 256, 0, st>>>(a, nullptr, hw, c, rs, (double*)ws);
+  if (pr.mean) img_chan_sum_kernel<true><<<g1, 256, 0, st>>>(a, nullptr, hw, c, rs, pr, (double*)ws);
+  else img_chan_sum_kernel<false><<<g1, 256, 0, st>>>(a, nullptr, hw, c, rs, pr, (double*)ws);
   int rc = check_launch("img_chan_sum_kernel");
   if (rc) return rc;
   se_fc_fwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse + SE_THREADS), st>>>(
@@ -529,9 +584,25 @@ extern "C" int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const f
   return check_launch("se_fc_fwd_kernel");
 }
 
-extern "C" int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c, int cse,
-                          const float* w1, const float* w2, const float* z1, const float* gate,
-                          float* addn, void* ws, void* stream) {
+extern "C" int pld_se_fwd(const float* a, int n, int hw, int c, int cse, const float* w1,
+                          const float* b1, const float* w2, const float* b2, float* pooled,
+                          float* z1, float* gate, void* ws, void* stream) {
+  return se_fwd_impl(a, SePro{}, n, hw, c, cse, w1, b1, w2, b2, pooled, z1, gate, ws, stream);
+}
+
+extern "C" int pld_se_fwd_bn(const float* x, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int act, int n, int hw, int c,
+                             int cse, const float* w1, const float* b1, const float* w2,
+                             const float* b2, float* pooled, float* z1, float* gate, void* ws,
+                             void* stream) {
+  PLD_CHECK_ARG(mean && invstd && gamma && beta, "pld_se_fwd_bn: incomplete BN prologue");
+  return se_fwd_impl(x, SePro{mean, invstd, gamma, beta, act}, n, hw, c, cse, w1, b1, w2, b2,
+                     pooled, z1, gate, ws, stream);
+}
+
+static int se_bwd_impl(const float* dy, const float* a, const SePro& pr, int n, int hw, int c,
+                       int cse, const float* w1, const float* w2, const float* z1,
+                       const float* gate, float* addn, void* ws, void* stream) {
   PLD_CHECK_ARG(dy && a && w1 && w2 && z1 && gate && addn && ws && n > 0 && hw > 0 && c > 0 &&
                     cse > 0,
                 "pld_se_bwd: bad args");
@@ -539,10 +610,27 @@ extern "C" int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c,
   hipStream_t st = as_stream(stream);
   const int rs = se_rsplit(n, hw, c);
   dim3 g1(n * rs, cdiv(c / 4, 256));
-  img_chan_sum_kernel<<<g1, 256, 0, st>>>(a, dy, hw, c, rs, (double*)ws);
+  if (pr.mean) img_chan_sum_kernel<true><<<g1, 256, 0, st>>>(a, dy, hw, c, rs, pr, (double*)ws);
+  else img_chan_sum_kernel<false><<<g1, 256, 0, st>>>(a, dy, hw, c, rs, pr, (double*)ws);
   int rc = check_launch("img_chan_sum_kernel(bwd)");
   if (rc) return rc;
   se_fc_bwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse), st>>>(
       (const double*)ws, rs, hw, c, cse, w1, w2, z1, gate, addn);
   return check_launch("se_fc_bwd_kernel");
+}
+
+extern "C" int pld_se_bwd(const float* dy, const float* a, int n, int hw, int c, int cse,
+                          const float* w1, const float* w2, const float* z1, const float* gate,
+                          float* addn, void* ws, void* stream) {
+  return se_bwd_impl(dy, a, SePro{}, n, hw, c, cse, w1, w2, z1, gate, addn, ws, stream);
+}
+
+extern "C" int pld_se_bwd_bn(const float* dy, const float* x, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, int act,
+                             int n, int hw, int c, int cse, const float* w1, const float* w2,
+                             const float* z1, const float* gate, float* addn, void* ws,
+                             void* stream) {
+  PLD_CHECK_ARG(mean && invstd && gamma && beta, "pld_se_bwd_bn: incomplete BN prologue");
+  return se_bwd_impl(dy, x, SePro{mean, invstd, gamma, beta, act}, n, hw, c, cse, w1, w2, z1,
+                     gate, addn, ws, stream);
 }

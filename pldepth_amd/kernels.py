@@ -504,20 +504,33 @@ def dwconv_dgrad(dy, wdw, k, s, pad_t, pad_l, dx, accumulate=False):
                            int(accumulate), stream())
 
 
-def se_fwd(a, w1, b1, w2, b2, pooled, z1, gate):
+def se_fwd(a, w1, b1, w2, b2, pooled, z1, gate, bn=None, act="swish"):
+    """bn = (mean, invstd, gamma, beta): `a` is the pre-BN tensor; the squeeze applies BN + act."""
     n, h, w, c = a.shape
     cse = w1.shape[-1]
     ws = workspace(lib().pld_se_workspace_size(n, h * w, c, cse), "se")
-    lib().pld_se_fwd(ptr(a), n, h * w, c, cse, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(pooled),
-                     ptr(z1), ptr(gate), ptr(ws), stream())
+    if bn is None:
+        lib().pld_se_fwd(ptr(a), n, h * w, c, cse, ptr(w1), ptr(b1), ptr(w2), ptr(b2),
+                         ptr(pooled), ptr(z1), ptr(gate), ptr(ws), stream())
+    else:
+        mu, inv, g, b = bn
+        lib().pld_se_fwd_bn(ptr(a), ptr(mu), ptr(inv), ptr(g), ptr(b), ACT[act], n, h * w, c,
+                            cse, ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(pooled), ptr(z1),
+                            ptr(gate), ptr(ws), stream())
 
 
-def se_bwd(dy, a, w1, w2, z1, gate, addn):
+def se_bwd(dy, a, w1, w2, z1, gate, addn, bn=None, act="swish"):
     n, h, w, c = a.shape
     cse = w1.shape[-1]
     ws = workspace(lib().pld_se_workspace_size(n, h * w, c, cse), "se")
-    lib().pld_se_bwd(ptr(dy), ptr(a), n, h * w, c, cse, ptr(w1), ptr(w2), ptr(z1), ptr(gate),
-                     ptr(addn), ptr(ws), stream())
+    if bn is None:
+        lib().pld_se_bwd(ptr(dy), ptr(a), n, h * w, c, cse, ptr(w1), ptr(w2), ptr(z1),
+                         ptr(gate), ptr(addn), ptr(ws), stream())
+    else:
+        mu, inv, g, b = bn
+        lib().pld_se_bwd_bn(ptr(dy), ptr(a), ptr(mu), ptr(inv), ptr(g), ptr(b), ACT[act], n,
+                            h * w, c, cse, ptr(w1), ptr(w2), ptr(z1), ptr(gate), ptr(addn),
+                            ptr(ws), stream())
 
 
 # -------------------------------------------------------------------------------- sampler

@@ -357,15 +357,19 @@ class EffNetFF:
         rows = B * oh * ow
         bn = blk["bn"]
         bn.stats_(A[n + "dw_pre"], rows, training)
-        bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
         F = self.frozen
-        K.se_fwd(A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
-                 F[blk["se_b1"]], F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]],
-                 blk["pooled"], blk["z1"], blk["gate"])
+        se_w = (F[blk["se_w1"]].view(blk["cexp"], blk["cse"]), F[blk["se_b1"]],
+                F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]])
         if training:
+            # the SE squeeze applies BN + swish to dw_pre on the fly and se_excite is written
+            # straight from dw_pre: the block's activation is never materialised
+            K.se_fwd(A[n + "dw_pre"], *se_w, blk["pooled"], blk["z1"], blk["gate"],
+                     bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="swish")
             bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "se_excite"], True, gate=blk["gate"],
                      hw=oh * ow)
         else:
+            bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
+            K.se_fwd(A[n + "activation"], *se_w, blk["pooled"], blk["z1"], blk["gate"])
             self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
         K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
                                  math=self._em(oh, ow)),
@@ -467,9 +471,10 @@ class EffNetFF:
                                    math=self._em(oh, ow)),
                        gp, blk["project"].w_dg, gse)
         F = self.frozen
-        K.se_bwd(gse, A[n + "activation"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
+        bn = blk["bn"]
+        K.se_bwd(gse, A[n + "dw_pre"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
                  F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), blk["z1"], blk["gate"],
-                 blk["addn"])
+                 blk["addn"], bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="swish")
         gdw = self._gpre_buf(A[n + "dw_pre"].shape)
         blk["bn"].bwd(A[n + "dw_pre"], gse, rows, "swish", gdw, gate=blk["gate"],
                       addn=blk["addn"], hw=oh * ow)

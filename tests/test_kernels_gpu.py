@@ -434,6 +434,44 @@ def test_se_fwd_bwd(cuda, n, h, w, c, cse):
     assert rel_err(da, a.grad) < 1e-4
 
 
+@pytest.mark.parametrize("n,h,w,c,cse", [(2, 7, 9, 96, 4), (3, 14, 14, 240, 10),
+                                         (2, 33, 29, 16, 4)])
+def test_se_with_bn_prologue(cuda, n, h, w, c, cse):
+    """pld_se_{fwd,bwd}_bn (SE squeeze of swish(BN(x)) computed on the fly from the pre-BN x)
+    against the fp64 restatement of BN + swish + SE."""
+    torch.manual_seed(c + 1)
+    x = torch.randn(n, h, w, c, dtype=torch.float64) * 2 + 0.3
+    mu = x.mean(dim=(0, 1, 2))
+    inv = 1.0 / torch.sqrt(x.var(dim=(0, 1, 2), unbiased=False) + 1e-3)
+    gam = torch.rand(c, dtype=torch.float64) + 0.5
+    bet = torch.randn(c, dtype=torch.float64) * 0.2
+    a = OE.swish((x - mu) * inv * gam + bet).detach().requires_grad_(True)
+    w1 = torch.randn(1, 1, c, cse, dtype=torch.float64) * 0.2
+    b1 = torch.randn(cse, dtype=torch.float64) * 0.1
+    w2 = torch.randn(1, 1, cse, c, dtype=torch.float64) * 0.2
+    b2 = torch.randn(c, dtype=torch.float64) * 0.1
+    an = a.permute(0, 3, 1, 2)
+    gate = torch.sigmoid(OE.conv(OE.swish(OE.conv(an.mean(dim=(2, 3), keepdim=True), w1, b1)),
+                                 w2, b2))
+    y_ref = (an * gate).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    bn = tuple(dev(t, cuda) for t in (mu, inv, gam, bet))
+    gx = dev(x, cuda)
+    gp, gz, gg = (torch.empty(n, c, device=cuda), torch.empty(n, cse, device=cuda),
+                  torch.empty(n, c, device=cuda))
+    W1, W2 = dev(w1.view(c, cse), cuda), dev(w2.view(cse, c), cuda)
+    K.se_fwd(gx, W1, dev(b1, cuda), W2, dev(b2, cuda), gp, gz, gg, bn=bn, act="swish")
+    torch.cuda.synchronize()
+    assert rel_err(gg, gate.view(n, c)) < 1e-5
+    addn = torch.empty(n, c, device=cuda)
+    gdy = dev(dy, cuda)
+    K.se_bwd(gdy, gx, W1, W2, gz, gg, addn, bn=bn, act="swish")
+    torch.cuda.synchronize()
+    da = gdy * gg.view(n, 1, 1, c) + addn.view(n, 1, 1, c)
+    assert rel_err(da, a.grad) < 1e-4
+
+
 # ------------------------------------------------------------------------------- sampler
 @pytest.mark.parametrize("ci", range(4))
 @pytest.mark.parametrize("strategy", ["thresh", "info", "pure", "masked"])
