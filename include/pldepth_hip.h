@@ -237,6 +237,12 @@ int pld_maxpool2d_bwd(const float* dy, const uint8_t* argmax, int n, int h, int 
 /* UpSampling2D(interpolation='bilinear') x2, half-pixel centres (pl_hourglass.py:62..94):
  * x [n][h][w][c] -> y [n][2h][2w][c];  bwd: dx [n][h][w][c] (=|+=) adjoint(dy) */
 int pld_upsample2x_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream);
+/* Same, with the decoder's training-mode BatchNormalization + Activation (pl_hourglass.py:88-90)
+ * applied to each tap as it is read: x is the pre-BN conv output, act as pld_bn_apply. mean == NULL
+ * is the plain upsample. */
+int pld_upsample2x_fwd_bn(const float* x, int n, int h, int w, int c, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, int act,
+                          float* y, void* stream);
 int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx, int accumulate,
                        void* stream);
 /* y = a * sample_scale[img] + b  (EfficientNet drop-connect Dropout(noise_shape=(N,1,1,1)) +

@@ -71,6 +71,7 @@ _SIGS = {
     "pld_maxpool2d_bwd": (I32, [P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32,
                                 P]),
     "pld_upsample2x_fwd": (I32, [P, I32, I32, I32, I32, P, P]),
+    "pld_upsample2x_fwd_bn": (I32, [P, I32, I32, I32, I32, P, P, P, P, I32, P, P]),
     "pld_upsample2x_bwd": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "pld_residual_add": (I32, [P, P, P, I32, I64, P, P]),
     "pld_scale_per_sample": (I32, [P, P, I32, I64, P, I32, P]),

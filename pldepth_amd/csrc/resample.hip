@@ -42,9 +42,19 @@ __device__ __forceinline__ void lerp_coords(int o, int in_size, int& lo, int& hi
   l = in - f;
 }
 
-template <int VW>
+// optional input prologue: the decoder's BN + ReLU applied to each tap on the fly (the
+// activation before the upsampling is never materialised in training)
+struct UpPro {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+};
+
+template <int VW, bool PRO>
 __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __restrict__ x, int n,
-                                                             int h, int w, int c,
+                                                             int h, int w, int c, UpPro pr,
                                                              float* __restrict__ y) {
   const int cv = c / VW;
   const int H2 = 2 * h, W2 = 2 * w;
@@ -67,6 +77,20 @@ __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __rest
     ld4<VW>(base + ((long)y0 * w + x1) * c, tr);
     ld4<VW>(base + ((long)y1 * w + x0) * c, bl);
     ld4<VW>(base + ((long)y1 * w + x1) * c, br);
+    if (PRO) {
+      float mu[VW], is[VW], ga[VW], be[VW];
+      ld4<VW>(pr.mean + q * VW, mu);
+      ld4<VW>(pr.invstd + q * VW, is);
+      ld4<VW>(pr.gamma + q * VW, ga);
+      ld4<VW>(pr.beta + q * VW, be);
+#pragma unroll
+      for (int u = 0; u < VW; ++u) {  // the bn_apply arithmetic, then the activation
+        tl[u] = act_fwd(pr.act, ((tl[u] - mu[u]) * is[u]) * ga[u] + be[u]);
+        tr[u] = act_fwd(pr.act, ((tr[u] - mu[u]) * is[u]) * ga[u] + be[u]);
+        bl[u] = act_fwd(pr.act, ((bl[u] - mu[u]) * is[u]) * ga[u] + be[u]);
+        br[u] = act_fwd(pr.act, ((br[u] - mu[u]) * is[u]) * ga[u] + be[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < VW; ++u) {
       const float top = tl[u] + (tr[u] - tl[u]) * xl;
@@ -178,12 +202,24 @@ using namespace pld;
 extern "C" int pld_upsample2x_fwd(const float* x, int n, int h, int w, int c, float* y,
                                   void* stream) {
   PLD_CHECK_ARG(x && y && n > 0 && h > 0 && w > 0 && c > 0, "pld_upsample2x_fwd: bad args");
+  return pld_upsample2x_fwd_bn(x, n, h, w, c, nullptr, nullptr, nullptr, nullptr, 0, y, stream);
+}
+
+extern "C" int pld_upsample2x_fwd_bn(const float* x, int n, int h, int w, int c,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* beta, int act, float* y, void* stream) {
+  PLD_CHECK_ARG(x && y && n > 0 && h > 0 && w > 0 && c > 0, "pld_upsample2x_fwd: bad args");
+  PLD_CHECK_ARG(!mean || (invstd && gamma && beta), "pld_upsample2x_fwd_bn: incomplete BN");
   hipStream_t st = as_stream(stream);
   const long total = (long)n * 4 * h * w * c;
-  if (c % 4 == 0)
-    upsample2x_fwd_kernel<4><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, y);
-  else
-    upsample2x_fwd_kernel<1><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, y);
+  const UpPro pr{mean, invstd, gamma, beta, act};
+  if (c % 4 == 0) {
+    if (mean) upsample2x_fwd_kernel<4, true><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y);
+    else upsample2x_fwd_kernel<4, false><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y);
+  } else {
+    if (mean) upsample2x_fwd_kernel<1, true><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y);
+    else upsample2x_fwd_kernel<1, false><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y);
+  }
   return check_launch("upsample2x_fwd_kernel");
 }
 

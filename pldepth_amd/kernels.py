@@ -442,9 +442,16 @@ def channel_affine_act(x, rows, c, scale, shift, act, y):
 
 
 # ------------------------------------------------------------------------------ resampling
-def upsample2x_fwd(x, y):
+def upsample2x_fwd(x, y, bn=None, act="none"):
+    """bn = (mean, invstd, gamma, beta): x is the pre-BN tensor; BN + act is applied to each
+    tap as it is read (the activation before the upsampling is never materialised)."""
     n, h, w, c = x.shape
-    lib().pld_upsample2x_fwd(ptr(x), n, h, w, c, ptr(y), stream())
+    if bn is None:
+        lib().pld_upsample2x_fwd(ptr(x), n, h, w, c, ptr(y), stream())
+    else:
+        mean, invstd, gamma, beta = bn
+        lib().pld_upsample2x_fwd_bn(ptr(x), n, h, w, c, ptr(mean), ptr(invstd), ptr(gamma),
+                                    ptr(beta), ACT[act], ptr(y), stream())
     return y
 
 

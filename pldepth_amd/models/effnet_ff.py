@@ -321,8 +321,14 @@ class EffNetFF:
             K.conv2d_fwd(args, conv.w_nat, conv.b, A[f"dec{i}_pre"])
             rows = B * h * w
             bn.stats_(A[f"dec{i}_pre"], rows, training)
-            bn.apply(A[f"dec{i}_pre"], rows, "relu", A[f"dec{i}_act"], training)
-            K.upsample2x_fwd(A[f"dec{i}_act"], A[f"dec{i}_up"])
+            if training:
+                # BN + ReLU applied as the upsampling reads its taps: dec{i}_act is never
+                # materialised (backward re-derives it from dec{i}_pre)
+                K.upsample2x_fwd(A[f"dec{i}_pre"], A[f"dec{i}_up"],
+                                 bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="relu")
+            else:
+                bn.apply(A[f"dec{i}_pre"], rows, "relu", A[f"dec{i}_act"], training)
+                K.upsample2x_fwd(A[f"dec{i}_act"], A[f"dec{i}_up"])
             h, w = 2 * h, 2 * w
             x, x2 = A[f"dec{i}_up"], (A[skip] if skip else None)
         pt, _ = same_pad(h, 3, 1)

@@ -335,6 +335,30 @@ def test_upsample2x(cuda, n, h, w, c):
     assert rel_err(dx, x.grad) < 1e-6
 
 
+@pytest.mark.parametrize("n,h,w,c", [(2, 5, 7, 8), (1, 4, 4, 3), (2, 14, 14, 144)])
+def test_upsample2x_bn_prologue(cuda, n, h, w, c):
+    """decoder training forward: BN + ReLU of the conv output applied inside the upsample"""
+    x = torch.randn(n, h, w, c, dtype=torch.float64)
+    gamma, beta = torch.rand(c, dtype=torch.float64) + 0.5, torch.randn(c, dtype=torch.float64)
+    rows = n * h * w
+    gx = dev(x, cuda)
+    gm, gi = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_stats(gx, rows, c, gm, gi)
+    mu, var = x.mean((0, 1, 2)), x.var((0, 1, 2), unbiased=False)
+    a = torch.relu((x - mu) / torch.sqrt(var + 1e-3) * gamma + beta)
+    y_ref = OE.up2(a.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    y = torch.empty(n, 2 * h, 2 * w, c, device=cuda)
+    K.upsample2x_fwd(gx, y, bn=(gm, gi, dev(gamma, cuda), dev(beta, cuda)), act="relu")
+    # the fused form must equal the two-pass form (bn_apply then upsample) to the last bit
+    act = torch.empty_like(gx)
+    K.bn_apply(gx, rows, c, gm, gi, dev(gamma, cuda), dev(beta, cuda), "relu", act)
+    y2 = torch.empty_like(y)
+    K.upsample2x_fwd(act, y2)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5
+    assert rel_err(y, y2) < 1e-6
+
+
 def test_residual_and_per_sample_scale(cuda):
     a = torch.randn(3, 4, 5, 8)
     b = torch.randn(3, 4, 5, 8)
