@@ -281,6 +281,116 @@ __global__ __launch_bounds__(256) void candidate_kernel(RankParams p) {
   }
 }
 
+// 8 < L <= 64: one wavefront per candidate list, lane j holding draw j. The sort is a rank
+// computation — position of j = #{k : g_k > g_j} + #{k : g_k == g_j, k > j}, exactly the
+// stable-ascending-then-reversed order of candidate_kernel — and ds_permute moves each element to
+// the lane of its position. Scores use the same fp32/fp64 operation order as candidate_kernel
+// (NumPy's 8-accumulator pairwise sum for 8 <= L <= 128), computed redundantly by every lane.
+__global__ __launch_bounds__(256) void candidate_wave_kernel(RankParams p) {
+  const int lane = threadIdx.x & 63;
+  const long total = (long)p.B * p.n_cand;
+  const int L = p.L;
+  const int HW = p.H * p.W;
+  for (long e = (long)blockIdx.x * 4 + (threadIdx.x >> 6); e < total; e += (long)gridDim.x * 4) {
+    const int b = (int)(e / p.n_cand);
+    float g = 0.0f;
+    int id = 0;
+    if (lane < L) {
+      const int nv = p.nvalid[b];
+      int d = p.draws[e * L + lane];
+      d = min(max(d, 0), max(nv - 1, 0));
+      id = p.valid_idx[(long)b * HW + d];
+      g = p.gt[(long)b * HW + id];
+    }
+    int rank = 0;
+    for (int k = 0; k < L; ++k) {  // wave-uniform trip count: every lane takes part in the shfl
+      const float gk = __shfl(g, k, 64);
+      rank += (gk > g) | ((gk == g) & (k > lane));
+    }
+    if (lane >= L) rank = lane;  // idle lanes keep their slot: the permutation stays 1:1
+    const float gs = __int_as_float(__builtin_amdgcn_ds_permute(rank << 2, __float_as_int(g)));
+    const int ids = __builtin_amdgcn_ds_permute(rank << 2, id);
+    if (lane < L)
+      reinterpret_cast<float2*>(p.cand + e * L * 2)[lane] = make_float2((float)ids, gs);
+    double sc = 0.0;
+    if (p.strategy == PLD_SAMPLER_MASKED || p.strategy == PLD_SAMPLER_THRESH) {
+      float acc = 0.0f;
+      float gj = __shfl(gs, 0, 64);
+      for (int j = 0; j + 1 < L; ++j) {
+        const float gj1 = __shfl(gs, j + 1, 64);
+        if (p.strategy == PLD_SAMPLER_THRESH && depth_relation32(gj, gj1) == 0)
+          acc = __fadd_rn(acc, -1000.0f);
+        acc = __fadd_rn(acc, fabsf(__fsub_rn(gj, gj1)));
+        gj = gj1;
+      }
+      sc = (double)acc;
+    } else if (p.strategy == PLD_SAMPLER_INFO) {
+      const float start = __fadd_rn(p.gt_minmax[2 * b], 0.001f);
+      const float stop = p.gt_minmax[2 * b + 1];
+      const float stepv = __fdiv_rn(__fsub_rn(stop, start), (float)L);
+      const float ev =
+          (lane == L - 1) ? stop : __fadd_rn(__fmul_rn((float)(lane + 1), stepv), start);
+      const float dd = __fsub_rn(gs, ev);
+      const float t = __fdiv_rn(__fmul_rn(dd, dd), ev);
+      // pairwise_sum32, 8 <= n <= 128 branch
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = __shfl(t, j, 64);
+      const int nfull = L - (L % 8);
+      int i = 8;
+      for (; i < nfull; i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], __shfl(t, i + j, 64));
+      float res = __fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3]));
+      res = __fadd_rn(res, __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+      for (; i < L; ++i) res = __fadd_rn(res, __shfl(t, i, 64));
+      sc = -(double)__fadd_rn(0.0f, res);
+      const float gn = __shfl(gs, min(lane + 1, 63), 64);
+      const int nz = __popcll(__ballot(lane + 1 < L && depth_relation32(gs, gn) == 0));
+      for (int k = 0; k < nz; ++k) sc = __dadd_rn(sc, -1000.0);
+    }
+    if (lane == 0) p.score[e] = sc;
+  }
+}
+
+// per-image top-R, spread over (B, n / 256) workgroups: every workgroup stages the image's n
+// scores in LDS and ranks 256 candidates against them, then copies the selected lists with all
+// threads (coalesced). Same rank definition as select_kernel.
+__global__ __launch_bounds__(256) void select_chunk_kernel(RankParams p) {
+  extern __shared__ double s_score[];
+  __shared__ int s_rank[256];
+  const int b = blockIdx.x;
+  const int n = p.n_cand;
+  const double* sb = p.score + (long)b * n;
+  for (int i = threadIdx.x; i < n; i += 256) s_score[i] = sb[i];
+  __syncthreads();
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  int rank = n;
+  if (i < n) {
+    const double si = s_score[i];
+    int r0 = 0, r1 = 0;
+    int j = 0;
+    for (; j + 1 < n; j += 2) {
+      const double s0 = s_score[j], s1 = s_score[j + 1];
+      r0 += (s0 > si) | ((s0 == si) & (j > i));
+      r1 += (s1 > si) | ((s1 == si) & (j + 1 > i));
+    }
+    if (j < n) r0 += (s_score[j] > si) | ((s_score[j] == si) & (j > i));
+    rank = r0 + r1;
+  }
+  s_rank[threadIdx.x] = rank;
+  __syncthreads();
+  const int L2 = 2 * p.L;
+  const int cnt = min(256, n - (int)blockIdx.y * 256);
+  for (int q = threadIdx.x; q < cnt * L2; q += 256) {
+    const int c = q / L2, k = q - c * L2;
+    const int rk = s_rank[c];
+    if (rk < p.R_out)
+      p.out[((long)b * p.R_out + rk) * L2 + k] =
+          p.cand[((long)b * n + blockIdx.y * 256 + c) * L2 + k];
+  }
+}
+
 // per-image top-R: rank of candidate i = #{j : (score_j, j) > (score_i, i)} (lexicographic);
 // the reference's argsort(scores)[::-1] order with ties broken toward the higher index
 __global__ __launch_bounds__(1024) void select_kernel(RankParams p) {
@@ -416,7 +526,8 @@ extern "C" int pld_sampler_rank(const float* gt, const int* valid_idx, const int
   const long total = (long)B * nc;
   const unsigned g = std::min<unsigned>(cdiv(total, 256), 8192);
   if (L <= 8) candidate_kernel<8><<<g, 256, 0, st>>>(p);
-  else if (L <= 64) candidate_kernel<64><<<g, 256, 0, st>>>(p);
+  else if (L <= 64)
+    candidate_wave_kernel<<<std::min<unsigned>(cdiv(total, 4), 16384), 256, 0, st>>>(p);
   else candidate_kernel<512><<<g, 256, 0, st>>>(p);
   int rc = check_launch("candidate_kernel");
   if (rc) return rc;
@@ -425,8 +536,12 @@ extern "C" int pld_sampler_rank(const float* gt, const int* valid_idx, const int
     copy_first_kernel<<<std::min<unsigned>(cdiv(n, 256), 4096), 256, 0, st>>>(p);
     return check_launch("copy_first_kernel");
   }
-  PLD_CHECK_ARG(sizeof(double) * (size_t)nc <= 160 * 1024,
+  PLD_CHECK_ARG(sizeof(double) * (size_t)nc <= 150 * 1024,
                 "pld_sampler_rank: %d candidates exceed the LDS selection buffer", nc);
-  select_kernel<<<B, 1024, sizeof(double) * nc, st>>>(p);
-  return check_launch("select_kernel");
+  if (nc <= 1024) {
+    select_kernel<<<B, 1024, sizeof(double) * nc, st>>>(p);
+    return check_launch("select_kernel");
+  }
+  select_chunk_kernel<<<dim3(B, cdiv(nc, 256)), 256, sizeof(double) * nc, st>>>(p);
+  return check_launch("select_chunk_kernel");
 }

@@ -521,6 +521,34 @@ def test_sampler_bit_exact_vs_oracle(cuda, golden, ci, strategy):
         np.testing.assert_array_equal(out[b].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("L,R", [(64, 1000), (20, 300), (9, 250), (64, 30)])
+@pytest.mark.parametrize("strategy", ["info", "thresh", "masked", "pure"])
+def test_sampler_stress_shapes_bit_exact(cuda, L, R, strategy):
+    """BASELINE cfg5 (448x448, L=64, R=1000: 5,000 Info candidates per image -> the wave-per-list
+    candidate kernel and the chunked top-R selection) and ragged L against the oracle, on 8-bit
+    depth codes (many tied depths and tied scores)."""
+    h, w, B = 448, 448, 2
+    rng = np.random.default_rng(L * 1000 + R)
+    gts = (np.round(rng.random((B, h, w)) * 255) / 255).astype(np.float32)
+    masks = (rng.random((B, h, w)) < 0.9).astype(np.float32)
+    nc = {"info": 5 * R, "thresh": int(R * 1.5), "masked": int(R * 1.5), "pure": int(R * 0.8)}
+    draws = np.stack([rng.integers(0, int(masks[b].sum()), (nc[strategy], L)) for b in range(B)])
+    draws = draws.astype(np.int32)
+    vi = torch.empty(B, h * w, dtype=torch.int32, device=cuda)
+    nv = torch.empty(B, dtype=torch.int32, device=cuda)
+    mm = torch.empty(B, 2, device=cuda)
+    ggt = dev(torch.from_numpy(gts), cuda)
+    K.sampler_compact(dev(torch.from_numpy(masks), cuda), ggt, vi, nv, mm)
+    refs = [S.sample_masked_point_batch(strategy, masks[b], gts[b], R, L, draws[b].reshape(-1))[0]
+            for b in range(B)]
+    out = torch.empty((B,) + refs[0].shape, device=cuda)
+    K.sampler_rank(ggt, vi, nv, mm, torch.from_numpy(draws).to(cuda).contiguous(), R, L,
+                   strategy, out)
+    torch.cuda.synchronize()
+    for b in range(B):
+        np.testing.assert_array_equal(out[b].cpu().numpy(), refs[b])
+
+
 @pytest.mark.parametrize("h,w", [(448, 448), (37, 53), (1, 5), (130, 129)])
 def test_sampler_compact_matches_np_where(cuda, h, w):
     """Valid-pixel lists == np.where(mask > 0) order (sampling.py:135), nvalid, whole-image gt
