@@ -35,7 +35,7 @@ struct RedParams {
   const float* addn;
   const float* res;  // residual added before the activation (ResNet / ReDWeb blocks), or NULL
   FastDiv dHW;
-  double* partial;  // [gridDim.x][C][2]
+  double* partial;  // [C][gridDim.x][2]
 };
 
 template <int VW>
@@ -164,12 +164,11 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         s1[u] += red[tid + j * ncv][VW + u];
       }
     }
-    double* out = p.partial + ((long)blockIdx.x * p.C + cv * VW) * 2;
+    // channel-major partials: the finalize kernel's per-channel read is one contiguous run
 #pragma unroll
-    for (int u = 0; u < VW; ++u) {
-      out[2 * u] = s0[u];
-      out[2 * u + 1] = s1[u];
-    }
+    for (int u = 0; u < VW; ++u)
+      *reinterpret_cast<double2*>(p.partial + (((long)(cv * VW + u)) * gridDim.x + blockIdx.x) * 2) =
+          make_double2(s0[u], s1[u]);
   }
 }
 
@@ -198,28 +197,32 @@ static int launch_reduce(int op, RedParams& p, hipStream_t st) {
   return check_launch("chan_reduce_kernel");
 }
 
-// ---- finalize kernels: one workgroup per channel sums that channel's nbx partials (strided
-// over the 256 threads, then a fixed-shape tree: deterministic, latency-parallel) ----
+// ---- finalize kernels: one workgroup per channel sums that channel's nbx partials (one
+// contiguous [nbx][2] run, coalesced 16-byte loads strided over the 256 threads, then a
+// fixed-shape wavefront butterfly and a 4-way LDS sum: deterministic, latency-parallel) ----
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ part, int nbx, int C,
                                                 int c, double& s, double& q) {
-  __shared__ double rs[256], rq[256];
+  __shared__ double rs[4], rq[4];
+  const double2* run = reinterpret_cast<const double2*>(part) + (long)c * nbx;
   double a = 0.0, b = 0.0;
   for (int i = threadIdx.x; i < nbx; i += 256) {
-    a += part[((long)i * C + c) * 2];
-    b += part[((long)i * C + c) * 2 + 1];
+    const double2 v = run[i];
+    a += v.x;
+    b += v.y;
   }
-  rs[threadIdx.x] = a;
-  rq[threadIdx.x] = b;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    rs[w] = a;
+    rq[w] = b;
+  }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      rs[threadIdx.x] += rs[threadIdx.x + o];
-      rq[threadIdx.x] += rq[threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  s = rs[0];
-  q = rq[0];
+  s = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+  q = (rq[0] + rq[1]) + (rq[2] + rq[3]);
 }
 
 __global__ __launch_bounds__(256) void stats_finalize_kernel(

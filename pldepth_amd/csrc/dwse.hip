@@ -337,6 +337,24 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
   }
 }
 
+// sum_k part[(img * rsplit + k) * c + ch] in k order, with up to 8 loads in flight (rsplit is
+// up to 32: one dependent load per k would leave the workgroup latency-bound)
+__device__ __forceinline__ double se_part_sum(const double* __restrict__ part, int img, int rsplit,
+                                              int c, int ch) {
+  const double* p = part + (long)img * rsplit * c + ch;
+  double s = 0.0;
+  int k = 0;
+  for (; k + 8 <= rsplit; k += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < rsplit; ++k) s += p[(long)k * c];
+  return s;
+}
+
 // forward excitation, one workgroup per image
 // SE excitation FCs (tiny: c <= 1152, cse <= 48 per image). Grid (image, SE_SLICES) of
 // 1024-thread workgroups: every workgroup rebuilds the image's full hidden vector (z1 fwd /
@@ -357,6 +375,7 @@ __device__ __forceinline__ void se_vecmat_cj(const float* v, const float* __rest
     float a0 = 0.f, a1 = 0.f;
     if (j < cse) {
       int ch = sl;
+#pragma unroll 4
       for (; ch + SE_CS < c; ch += 2 * SE_CS) {
         a0 += v[ch] * w[(long)ch * cse + j];
         a1 += v[ch + SE_CS] * w[(long)(ch + SE_CS) * cse + j];
@@ -380,6 +399,7 @@ __device__ __forceinline__ void se_vecmat_jc(const float* v, const float* __rest
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int j = wave; j < cse; j += SE_THREADS / 64) {
     float acc = 0.f;
+#pragma unroll 4
     for (int ch = lane; ch < c; ch += 64) acc += v[ch] * w[(long)j * c + ch];
     acc = wave_sum(acc);
     if (lane == 0) out[j] = acc;
@@ -401,8 +421,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_fwd_kernel(const double* __r
   float* red = sh + cse;      // [SE_THREADS]
   const int img = blockIdx.x, slice = blockIdx.y;
   for (int ch = threadIdx.x; ch < c; ch += SE_THREADS) {
-    double s = 0.0;
-    for (int k = 0; k < rsplit; ++k) s += part[((long)img * rsplit + k) * c + ch];
+    const double s = se_part_sum(part, img, rsplit, c, ch);
     sp[ch] = (float)(s / (double)hw);
   }
   __syncthreads();
@@ -420,6 +439,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_fwd_kernel(const double* __r
   const int cb = slice * per, ce = min(c, cb + per);
   for (int ch = cb + threadIdx.x; ch < ce; ch += SE_THREADS) {
     float acc = b2[ch];
+#pragma unroll 8
     for (int j = 0; j < cse; ++j) acc += sh[j] * w2[(long)j * c + ch];
     gate[(long)img * c + ch] = sigmoidf_(acc);
   }
@@ -439,8 +459,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
   float* dz1 = sm + c;   // [cse]
   const int img = blockIdx.x, slice = blockIdx.y;
   for (int ch = threadIdx.x; ch < c; ch += SE_THREADS) {
-    double s = 0.0;
-    for (int k = 0; k < rsplit; ++k) s += part[((long)img * rsplit + k) * c + ch];
+    const double s = se_part_sum(part, img, rsplit, c, ch);
     const float g = gate[(long)img * c + ch];
     dz2[ch] = (float)s * g * (1.f - g);
   }
@@ -458,6 +477,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
   const int cb = slice * per, ce = min(c, cb + per);
   for (int ch = cb + threadIdx.x; ch < ce; ch += SE_THREADS) {
     float acc = 0.f;
+#pragma unroll 8
     for (int j = 0; j < cse; ++j) acc += dz1[j] * w1[(long)ch * cse + j];
     addn[(long)img * c + ch] = acc / (float)hw;
   }
