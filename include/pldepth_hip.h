@@ -133,7 +133,8 @@ enum { PLD_SCHED_X3 = 0, PLD_SCHED_X3_SPLIT = 1, PLD_SCHED_X3_PATCH = 2, PLD_SCH
 int pld_conv_schedule_class(int math, int idx);
 /* which kernel family a conv call runs (mode 0 = fwd, 1 = dgrad, 2 = wgrad) for its math and
  * tile: PLD_KIND_FP32 (v_mfma_f32_32x32x2_f32), PLD_KIND_BF16X3 (v_mfma_f32_32x32x16_bf16 x3) or
- * PLD_KIND_DIRECT (single-output-channel VALU kernels); -1 on bad arguments. For roofline
+ * PLD_KIND_DIRECT (VALU kernels: single-output-channel 3x3 convs, thin 1x1 convs with GEMM K <= 48,
+ * K x N <= 4096 — HBM-bound); -1 on bad arguments. For roofline
  * accounting (each family has its own peak). */
 enum { PLD_KIND_FP32 = 0, PLD_KIND_BF16X3 = 1, PLD_KIND_DIRECT = 2 };
 int pld_conv_kernel_kind(const pld_conv_args* a, int mode);

@@ -670,6 +670,10 @@ extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float*
                                  int accumulate, void* ws, void* stream);
 
 // bf16x3 kernels (conv_x3.hip)
+extern "C" int pld__thin_ok(int K, int N);
+extern "C" int pld__thin_geom(const pld_conv_args* a);
+extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias, float* out,
+                              long M, int K, int N, int acc, void* stream);
 extern "C" int pld__x3_num_cfg(void);
 extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int* occ);
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
@@ -911,6 +915,10 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   PLD_CHECK_ARG(w_ohwi && y, "pld_conv2d_fwd: null w/y");
   if (pld__skinny_eligible(a) && aligned16(a->x1))
     return pld__skinny_fwd(a, w_ohwi, bias, y, accumulate, stream);
+  if (pld__thin_geom(a) && pld__thin_ok(a->c1, a->cout) && aligned16(a->x1) && aligned16(y) &&
+      aligned16(w_ohwi))
+    return pld__thin_gemm(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, a->c1, a->cout,
+                          accumulate, stream);
   p.bmat = w_ohwi;
   p.bsplit = (const float*)a->w_split;
   p.M = a->n * a->oh * a->ow;
@@ -950,6 +958,9 @@ extern "C" int pld_conv_schedule_class(int math, int idx) {
 extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
   if (!a || mode < 0 || mode > 2) return -1;
   if (pld__skinny_eligible(a) && !(mode == 1 && (a->sh != 1 || a->sw != 1)))
+    return PLD_KIND_DIRECT;
+  if (mode != 2 && pld__thin_geom(a) &&
+      (mode == 0 ? pld__thin_ok(a->c1, a->cout) : pld__thin_ok(a->cout, a->c1)))
     return PLD_KIND_DIRECT;
   bool geom, x3;
   int t;
@@ -1051,6 +1062,11 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   }
   if (pld__skinny_eligible(a) && aligned16(dx1))
     return pld__skinny_dgrad(a, dy, w_dgrad, dx1, accumulate1, stream);
+  // 1x1: w_dgrad is [cin][cout], dx = dy . w_dgrad^T
+  if (pld__thin_geom(a) && pld__thin_ok(a->cout, a->c1) && aligned16(dy) && aligned16(dx1) &&
+      aligned16(w_dgrad))
+    return pld__thin_gemm(dy, w_dgrad, nullptr, dx1, (long)a->n * a->h * a->w, a->cout, a->c1,
+                          accumulate1, stream);
   // dx[img][iy][ix][ci] = sum_{ty,tx,co} dy[img][iy+ty-pt'][ix+tx-pl'][co] * Wd[ci][ty][tx][co]
   // with pt' = kh-1-pt and the output spatial = the forward input spatial.
   pld_conv_args g = *a;

@@ -1,0 +1,138 @@
+// Thin 1x1 convolutions: out[m][n] = sum_k a[m][k] * b[n][k] with a small reduction (K <= 48, K % 8
+// == 0, N <= 256) — the EfficientNet expand / project convs of the early stages
+// (pl_hourglass.py:52-57 via Keras EfficientNetB0: 16->96, 24->144, 40->240 expand; 96->24,
+// 144->24, 240->40 project) and their data-gradients. These are HBM-bound (2-9 FMAs per byte),
+// so an MFMA tile buys nothing: the 64x32 / 256x32 MFMA tiles re-read `a` once per N tile and
+// reach ~3.5 TB/s on them. Here a 256-thread workgroup owns 64 consecutive rows (one contiguous
+// 64*K-float block of `a`, read fully coalesced and transposed through LDS so each lane holds
+// its row in VGPRs); its 4 waves split the output columns, the filter row of each column is
+// wave-uniform (scalar loads: the FMAs take it as an SGPR operand), and the outputs go back
+// through LDS in CH-column chunks so every store instruction writes whole 32/64-byte row
+// segments. Exact fp32 fmaf chains in k order.
+#include "common.h"
+#include "conv_common.h"
+
+namespace pld {
+
+constexpr int THIN_PAD = 4;  // LDS row padding (floats): spreads the lane-per-row reads over banks
+
+template <int KR, int CH>
+__global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      const float* __restrict__ bias,
+                                                      float* __restrict__ out, int M, int N,
+                                                      int acc) {
+  constexpr int LA = KR + THIN_PAD;  // LDS row stride of the staged a tile
+  constexpr int LO = CH + THIN_PAD;  // LDS row stride of a wave's output chunk
+  __shared__ __attribute__((aligned(16))) float sa[64 * LA];
+  __shared__ __attribute__((aligned(16))) float so[4][64 * LO];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar filter loads
+  const long m0 = (long)blockIdx.x * 64;
+  const int rows = (int)min(64L, (long)M - m0);
+  // stage the contiguous [rows][KR] block of a: float4 index e = tid + 256 j
+  constexpr int NV = 64 * KR / 4;
+  const float4* src = reinterpret_cast<const float4*>(a + m0 * KR);
+  const int nv = rows * KR / 4;
+#pragma unroll
+  for (int j = 0; j < (NV + 255) / 256; ++j) {
+    const int e = tid + 256 * j;
+    if (e < NV) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nv) v = src[e];
+      const int r = (4 * e) / KR, c = (4 * e) % KR;
+      *reinterpret_cast<float4*>(sa + r * LA + c) = v;
+    }
+  }
+  __syncthreads();
+  float x[KR];
+#pragma unroll
+  for (int k = 0; k < KR; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(sa + lane * LA + k);
+    x[k] = v.x; x[k + 1] = v.y; x[k + 2] = v.z; x[k + 3] = v.w;
+  }
+  // the 4 waves share the 64 rows and take CH-column chunks round-robin; from here on each wave
+  // only touches its own staging buffer (in-order LDS within a wave: no workgroup barrier)
+  float* sw = so[wave];
+  for (int n0 = wave * CH; n0 < N; n0 += 4 * CH) {
+    float o[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const float* br = b + (long)(n0 + j) * KR;  // wave-uniform row: scalar loads
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < KR; ++k) s = fmaf(x[k], br[k], s);
+      o[j] = bias ? s + bias[n0 + j] : s;
+    }
+#pragma unroll
+    for (int j = 0; j < CH; j += 4)
+      *reinterpret_cast<float4*>(sw + lane * LO + j) = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    __builtin_amdgcn_wave_barrier();
+    // rows x CH chunk: CH/4 lanes per row, 64 / (CH/4) rows per store instruction
+    constexpr int QPR = CH / 4;
+#pragma unroll
+    for (int j = 0; j < QPR; ++j) {
+      const int e = lane + 64 * j;
+      const int r = e / QPR, q = e % QPR;
+      if (r < rows) {
+        float4 v = *reinterpret_cast<const float4*>(sw + r * LO + 4 * q);
+        float4* d = reinterpret_cast<float4*>(out + (m0 + r) * N + n0 + 4 * q);
+        if (acc) v = add4(v, *d);
+        *d = v;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int KR>
+static void thin_launch(const float* a, const float* b, const float* bias, float* out, int M,
+                        int N, int acc, hipStream_t st) {
+  const unsigned grid = (unsigned)cdiv(M, 64);
+  if (N % 16 == 0 && N >= 128) thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
+  else thin1x1_kernel<KR, 8><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
+}
+
+static bool thin_kr_ok(int kr) { return kr % 8 == 0 && kr >= 8 && kr <= 48; }
+
+}  // namespace pld
+
+using namespace pld;
+
+// (K, N) of the GEMM a thin 1x1 conv runs: fwd K = cin, N = cout; dgrad K = cout, N = cin
+extern "C" int pld__thin_ok(int K, int N) {
+  static const int off = [] {
+    const char* e = getenv("PLD_NO_THIN");  // debug knob: route everything to the MFMA tiles
+    return e && e[0] == '1';
+  }();
+  if (off || N % 8 != 0 || !thin_kr_ok(K)) return 0;
+  // K x N <= 4096: above it (40 -> 240, 40 -> 144) the per-lane FMA chains outlast the HBM time
+  // and the MFMA tiles are as fast or faster (measured, profiles/r01_conv_table.txt)
+  return N <= 256 && K * N <= 4096;
+}
+
+// 1x1, stride 1, unpadded, single source, no prologue
+extern "C" int pld__thin_geom(const pld_conv_args* a) {
+  return a && a->kh == 1 && a->kw == 1 && a->sh == 1 && a->sw == 1 && a->pad_t == 0 &&
+         a->pad_l == 0 && a->c2 == 0 && a->x2 == nullptr && a->in_scale == nullptr &&
+         a->oh == a->h && a->ow == a->w;
+}
+
+extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias, float* out,
+                              long M, int K, int N, int acc, void* stream) {
+  PLD_CHECK_ARG(a && b && out && M > 0 && aligned16(a) && aligned16(out) && aligned16(b),
+                "thin1x1: bad args");
+  PLD_CHECK_ARG(M * (long)(K > N ? K : N) < (1L << 31), "thin1x1: tensor too large");
+  PLD_CHECK_ARG(pld__thin_ok(K, N), "thin1x1: unsupported K=%d N=%d", K, N);
+  hipStream_t st = as_stream(stream);
+  const int m = (int)M;
+  switch (K) {
+    case 8: thin_launch<8>(a, b, bias, out, m, N, acc, st); break;
+    case 16: thin_launch<16>(a, b, bias, out, m, N, acc, st); break;
+    case 24: thin_launch<24>(a, b, bias, out, m, N, acc, st); break;
+    case 32: thin_launch<32>(a, b, bias, out, m, N, acc, st); break;
+    case 40: thin_launch<40>(a, b, bias, out, m, N, acc, st); break;
+    default: thin_launch<48>(a, b, bias, out, m, N, acc, st); break;
+  }
+  return check_launch("thin1x1_kernel");
+}

@@ -705,3 +705,40 @@ def test_bn_add_forward_backward(cuda, rows, c, act):
     assert rel_err(dres - 2.0, rr.grad) < 1e-5
     assert rel_err(dg, gr.grad) < 1e-5
     assert rel_err(db, br.grad) < 1e-5
+
+
+# thin 1x1 convs (csrc/thin.hip): K <= 48, VALU with the filter in SGPRs; ragged
+# 64-row tails, every K instance, CH 8 and 16 column chunks, accumulate, fwd bias
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 7, 9, 16, 96), (1, 11, 13, 24, 144),
+                                            (1, 5, 5, 40, 96), (2, 9, 9, 96, 24),
+                                            (1, 6, 7, 144, 24), (3, 5, 5, 32, 16),
+                                            (1, 8, 8, 8, 40), (1, 3, 3, 48, 64),
+                                            (1, 64, 64, 64, 8)])
+def test_thin_1x1_conv(cuda, n, h, w, cin, cout):
+    torch.manual_seed(cin * 1000 + cout)
+    x = torch.randn(n, h, w, cin, dtype=torch.float64)
+    wt = torch.randn(1, 1, cin, cout, dtype=torch.float64) / np.sqrt(cin)
+    b = torch.randn(cout, dtype=torch.float64)
+    y_ref = torch.einsum("nhwc,cd->nhwd", x, wt[0, 0]) + b
+    dy = torch.randn(n, h, w, cout, dtype=torch.float64)
+    dx_ref = torch.einsum("nhwd,cd->nhwc", dy, wt[0, 0])
+    gx, gw = dev(x, cuda), dev(wt, cuda)
+    args = K.conv_args(gx, None, 1, 1, 1, 0, 0, h, w, cout, math="fp32")
+    lib = _lib.lib()
+    thin_fwd = cin % 8 == 0 and cin <= 48 and cout % 8 == 0 and cin * cout <= 4096
+    thin_dg = cout % 8 == 0 and cout <= 48 and cin % 8 == 0 and cin * cout <= 4096
+    assert thin_fwd or thin_dg
+    # PLD_KIND_DIRECT (2) = the thin path
+    assert (lib.pld_conv_kernel_kind(C.byref(args), 0) == 2) == thin_fwd
+    assert (lib.pld_conv_kernel_kind(C.byref(args), 1) == 2) == thin_dg
+    y = torch.empty(n, h, w, cout, device=cuda)
+    K.conv2d_fwd(args, K.filter_to_native(gw), dev(b, cuda), y)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
+    K.conv2d_fwd(args, K.filter_to_native(gw), dev(b, cuda), y, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, 2 * y_ref) < 1e-5
+    dx = torch.full_like(gx, 0.25)
+    K.conv2d_dgrad(args, dev(dy, cuda), K.filter_to_dgrad(gw), dx, None, acc1=True)
+    torch.cuda.synchronize()
+    assert rel_err(dx - 0.25, dx_ref) < 1e-5, rel_err(dx - 0.25, dx_ref)
