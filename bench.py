@@ -112,7 +112,7 @@ def conv_roofline(prof, traffic_file):
     return {
         "bound": "mfma",
         "kernel": "conv family: conv_x3_kernel / conv_x3_patch* (bf16x3 MFMA) + "
-                  "conv_igemm_kernel (fp32 MFMA) + direct Cout=1 kernels; fwd/dgrad/wgrad",
+                  "conv_igemm_kernel (fp32 MFMA) + direct VALU kernels (Cout=1 3x3, thin 1x1); fwd/dgrad/wgrad",
         "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "TFLOP/s",
         "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
         "flops_per_step": fl,

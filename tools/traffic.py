@@ -12,7 +12,7 @@ import csv
 import json
 import os
 
-CONV_MAIN = ("conv_igemm_kernel", "conv_x3_kernel", "conv_x3_patch", "skinny_fwd_kernel",
+CONV_MAIN = ("conv_igemm_kernel", "conv_x3_kernel", "conv_x3_patch", "thin1x1_kernel", "skinny_fwd_kernel",
              "skinny_dgrad_kernel", "skinny_wgrad_kernel")
 CONV_KERNELS = CONV_MAIN + ("splitk_", "stride_scatter_kernel", "skinny_wgrad_reduce_kernel")
 
