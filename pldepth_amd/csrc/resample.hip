@@ -55,18 +55,20 @@ struct UpPro {
 template <int VW, bool PRO>
 __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __restrict__ x, int n,
                                                              int h, int w, int c, UpPro pr,
-                                                             float* __restrict__ y) {
-  const int cv = c / VW;
-  const int H2 = 2 * h, W2 = 2 * w;
-  const long total = (long)n * H2 * W2 * cv;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(e % cv);
-    long t = e / cv;
-    const int ox = (int)(t % W2);
-    t /= W2;
-    const int oy = (int)(t % H2);
-    const int img = (int)(t / H2);
+                                                             float* __restrict__ y, FastDiv dCV,
+                                                             FastDiv dW2, FastDiv dH2) {
+  // 32-bit index math through multiply-high dividers (the host checks total < 2^31): 64-bit
+  // div/mod is a long instruction sequence per element
+  const uint32_t total = (uint32_t)n * dH2.d * dW2.d * dCV.d;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    const uint32_t t = dCV.div(e);
+    const int q = (int)(e - t * dCV.d);
+    const uint32_t t2 = dW2.div(t);
+    const int ox = (int)(t - t2 * dW2.d);
+    const uint32_t img_u = dH2.div(t2);
+    const int oy = (int)(t2 - img_u * dH2.d);
+    const int img = (int)img_u;
     int y0, y1, x0, x1;
     float yl, xl;
     lerp_coords(oy, h, y0, y1, yl);
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __rest
       const float bot = bl[u] + (br[u] - bl[u]) * xl;
       o[u] = top + (bot - top) * yl;
     }
-    st4<VW>(y + e * VW, o);
+    st4<VW>(y + (long)e * VW, o);
   }
 }
 
@@ -114,18 +116,19 @@ __device__ __forceinline__ int adj_taps(int k, int s, int (&o)[4], float (&wt)[4
 template <int VW>
 __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const float* __restrict__ dy, int n,
                                                              int h, int w, int c,
-                                                             float* __restrict__ dx, int acc) {
-  const int cv = c / VW;
+                                                             float* __restrict__ dx, int acc,
+                                                             FastDiv dCV, FastDiv dW, FastDiv dH) {
   const int W2 = 2 * w;
-  const long total = (long)n * h * w * cv;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(e % cv);
-    long t = e / cv;
-    const int kx = (int)(t % w);
-    t /= w;
-    const int ky = (int)(t % h);
-    const int img = (int)(t / h);
+  const uint32_t total = (uint32_t)n * dH.d * dW.d * dCV.d;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    const uint32_t t = dCV.div(e);
+    const int q = (int)(e - t * dCV.d);
+    const uint32_t t2 = dW.div(t);
+    const int kx = (int)(t - t2 * dW.d);
+    const uint32_t img_u = dH.div(t2);
+    const int ky = (int)(t2 - img_u * dH.d);
+    const int img = (int)img_u;
     int oy[4], ox[4];
     float wy[4], wx[4];
     const int ny = adj_taps(ky, h, oy, wy);
@@ -149,11 +152,11 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const float* __rest
     }
     if (acc) {
       float old[VW];
-      ld4<VW>(dx + e * VW, old);
+      ld4<VW>(dx + (long)e * VW, old);
 #pragma unroll
       for (int u = 0; u < VW; ++u) s[u] += old[u];
     }
-    st4<VW>(dx + e * VW, s);
+    st4<VW>(dx + (long)e * VW, s);
   }
 }
 
@@ -168,6 +171,26 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
     float v = a[e] * s;
     if (b) v += b[e];
     if (acc) v += y[e];
+    y[e] = v;
+  }
+}
+
+// float4 form (per % 4 == 0, 16-byte aligned, total < 2^33): 32-bit index math, the per-sample
+// scale's image index through a multiply-high divider
+__global__ __launch_bounds__(256) void residual4_kernel(const float4* __restrict__ a,
+                                                        const float* __restrict__ sc,
+                                                        const float4* __restrict__ b,
+                                                        FastDiv dPer4, uint32_t total4,
+                                                        float4* __restrict__ y) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total4;
+       e += gridDim.x * blockDim.x) {
+    const float s = sc ? sc[dPer4.div(e)] : 1.f;
+    const float4 u = a[e];
+    float4 v = make_float4(u.x * s, u.y * s, u.z * s, u.w * s);
+    if (b) {
+      const float4 w = b[e];
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
     y[e] = v;
   }
 }
@@ -212,13 +235,17 @@ extern "C" int pld_upsample2x_fwd_bn(const float* x, int n, int h, int w, int c,
   PLD_CHECK_ARG(!mean || (invstd && gamma && beta), "pld_upsample2x_fwd_bn: incomplete BN");
   hipStream_t st = as_stream(stream);
   const long total = (long)n * 4 * h * w * c;
+  PLD_CHECK_ARG(total < (1L << 31), "pld_upsample2x_fwd: tensor too large for 32-bit indexing");
   const UpPro pr{mean, invstd, gamma, beta, act};
+  const FastDiv dW2((uint32_t)(2 * w)), dH2((uint32_t)(2 * h));
   if (c % 4 == 0) {
-    if (mean) upsample2x_fwd_kernel<4, true><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y);
-    else upsample2x_fwd_kernel<4, false><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y);
+    const FastDiv dCV((uint32_t)(c / 4));
+    if (mean) upsample2x_fwd_kernel<4, true><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
+    else upsample2x_fwd_kernel<4, false><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
   } else {
-    if (mean) upsample2x_fwd_kernel<1, true><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y);
-    else upsample2x_fwd_kernel<1, false><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y);
+    const FastDiv dCV((uint32_t)c);
+    if (mean) upsample2x_fwd_kernel<1, true><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
+    else upsample2x_fwd_kernel<1, false><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
   }
   return check_launch("upsample2x_fwd_kernel");
 }
@@ -228,10 +255,14 @@ extern "C" int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, f
   PLD_CHECK_ARG(dy && dx && n > 0 && h > 0 && w > 0 && c > 0, "pld_upsample2x_bwd: bad args");
   hipStream_t st = as_stream(stream);
   const long total = (long)n * h * w * c;
+  PLD_CHECK_ARG(4 * total < (1L << 31), "pld_upsample2x_bwd: tensor too large for 32-bit indexing");
+  const FastDiv dW((uint32_t)w), dH((uint32_t)h);
   if (c % 4 == 0)
-    upsample2x_bwd_kernel<4><<<grid_for(total / 4), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate);
+    upsample2x_bwd_kernel<4><<<grid_for(total / 4), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate,
+                                                                  FastDiv((uint32_t)(c / 4)), dW, dH);
   else
-    upsample2x_bwd_kernel<1><<<grid_for(total), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate);
+    upsample2x_bwd_kernel<1><<<grid_for(total), 256, 0, st>>>(dy, n, h, w, c, dx, accumulate,
+                                                              FastDiv((uint32_t)c), dW, dH);
   return check_launch("upsample2x_bwd_kernel");
 }
 
@@ -239,6 +270,14 @@ extern "C" int pld_residual_add(const float* a, const float* sample_scale, const
                                 int64_t elems_per_img, float* y, void* stream) {
   PLD_CHECK_ARG(a && y && n > 0 && elems_per_img > 0, "pld_residual_add: bad args");
   const long total = (long)n * elems_per_img;
+  if (elems_per_img % 4 == 0 && total / 4 < (1L << 31) && aligned16(a) && aligned16(y) &&
+      (!b || aligned16(b))) {
+    residual4_kernel<<<grid_for(total / 4), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(a), sample_scale, reinterpret_cast<const float4*>(b),
+        FastDiv((uint32_t)(elems_per_img / 4)), (uint32_t)(total / 4),
+        reinterpret_cast<float4*>(y));
+    return check_launch("residual4_kernel");
+  }
   residual_kernel<<<grid_for(total), 256, 0, as_stream(stream)>>>(a, sample_scale, b,
                                                                   elems_per_img, total, y, 0);
   return check_launch("residual_kernel");

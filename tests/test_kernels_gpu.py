@@ -370,6 +370,21 @@ def test_residual_and_per_sample_scale(cuda):
     torch.testing.assert_close(y.cpu(), 2 * a * sc.view(3, 1, 1, 1) + b)
 
 
+@pytest.mark.parametrize("shape", [(3, 4, 5, 8), (2, 3, 5, 3), (4, 7, 7, 24)])
+def test_residual_inplace_vector_and_scalar_paths(cuda, shape):
+    """float4 path (per-image size % 4 == 0) and the scalar path, in place (y is a) as the
+    engine calls it, with and without the per-sample drop-connect scale."""
+    a = torch.randn(*shape)
+    b = torch.randn(*shape)
+    sc = torch.rand(shape[0]) + 0.5
+    ga = a.to(cuda)
+    K.residual_add(ga, sc.to(cuda), b.to(cuda), ga)
+    torch.testing.assert_close(ga.cpu(), a * sc.view(-1, 1, 1, 1) + b)
+    gb = a.to(cuda)
+    K.residual_add(gb, None, b.to(cuda), gb)
+    torch.testing.assert_close(gb.cpu(), a + b)
+
+
 # ------------------------------------------------------------------------- depthwise / SE
 @pytest.mark.parametrize("n,h,w,c,k,s", [(2, 12, 12, 16, 3, 1), (2, 12, 10, 24, 3, 2),
                                          (1, 14, 14, 40, 5, 2), (2, 7, 7, 8, 5, 1),
