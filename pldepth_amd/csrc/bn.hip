@@ -289,33 +289,35 @@ struct ApplyParams {
   float* y;
 };
 
+// The host sizes the grid so that its thread count is a multiple of C / VW: every thread's
+// elements then share one channel group, and the per-channel parameters are loaded once per
+// thread instead of once per element (ew_grid_c).
 template <int VW>
 __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
   const long nv = p.rows * p.C / VW;
   const int CV = p.C / VW;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nv;
-       e += (long)gridDim.x * blockDim.x) {
-    const long r = (long)p.dCV.div((uint32_t)e);
-    const int c0 = (int)(e - r * CV) * VW;
-    float xv[VW], a[VW], b[VW], g[VW];
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nv) return;
+  const int c0 = (int)(e - (long)p.dCV.div((uint32_t)e) * CV) * VW;
+  float mu[VW], is[VW], ga[VW], be[VW];
+  if (p.mean) {
+    ld<VW>(p.mean + c0, mu);
+    ld<VW>(p.invstd + c0, is);
+    ld<VW>(p.gamma + c0, ga);
+    ld<VW>(p.beta + c0, be);
+  } else {
+    ld<VW>(p.scale + c0, mu);
+    ld<VW>(p.shift + c0, is);
+  }
+  for (; e < nv; e += (long)gridDim.x * blockDim.x) {
+    float xv[VW], g[VW];
     ld<VW>(p.x + e * VW, xv);
     if (p.mean) {
-      float mu[VW], is[VW], ga[VW], be[VW];
-      ld<VW>(p.mean + c0, mu);
-      ld<VW>(p.invstd + c0, is);
-      ld<VW>(p.gamma + c0, ga);
-      ld<VW>(p.beta + c0, be);
 #pragma unroll
-      for (int u = 0; u < VW; ++u) {
-        a[u] = xv[u] - mu[u];
-        b[u] = is[u];
-        xv[u] = (a[u] * b[u]) * ga[u] + be[u];
-      }
+      for (int u = 0; u < VW; ++u) xv[u] = ((xv[u] - mu[u]) * is[u]) * ga[u] + be[u];
     } else {
-      ld<VW>(p.scale + c0, a);
-      ld<VW>(p.shift + c0, b);
 #pragma unroll
-      for (int u = 0; u < VW; ++u) xv[u] = xv[u] * a[u] + b[u];
+      for (int u = 0; u < VW; ++u) xv[u] = xv[u] * mu[u] + is[u];
     }
     if (p.res) {
       float rv[VW];
@@ -325,7 +327,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
     }
 #pragma unroll
     for (int u = 0; u < VW; ++u) g[u] = 1.f;
-    if (p.gate) ld<VW>(p.gate + (long)p.dHW.div((uint32_t)r) * p.C + c0, g);
+    if (p.gate) {
+      const long r = (long)p.dCV.div((uint32_t)e);
+      ld<VW>(p.gate + (long)p.dHW.div((uint32_t)r) * p.C + c0, g);
+    }
 #pragma unroll
     for (int u = 0; u < VW; ++u) xv[u] = act_fwd(p.act, xv[u]) * g[u];
     if constexpr (VW == 4)
@@ -361,22 +366,25 @@ template <int VW>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
   const long nv = p.rows * p.C / VW;
   const int CV = p.C / VW;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nv;
-       e += (long)gridDim.x * blockDim.x) {
-    const long r = (long)p.dCV.div((uint32_t)e);
-    const int c0 = (int)(e - r * CV) * VW;
-    float xv[VW], dv[VW], mu[VW], is[VW], ga[VW], be[VW], k1[VW], k2[VW], g[VW], a[VW];
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nv) return;
+  // one channel group per thread (grid from ew_grid_c): parameters loaded once
+  const int c0 = (int)(e - (long)p.dCV.div((uint32_t)e) * CV) * VW;
+  float mu[VW], is[VW], ga[VW], be[VW], k1[VW], k2[VW];
+  ld<VW>(p.mean + c0, mu);
+  ld<VW>(p.invstd + c0, is);
+  ld<VW>(p.gamma + c0, ga);
+  ld<VW>(p.beta + c0, be);
+  ld<VW>(p.k12 + c0, k1);
+  ld<VW>(p.k12 + p.C + c0, k2);
+  for (; e < nv; e += (long)gridDim.x * blockDim.x) {
+    float xv[VW], dv[VW], g[VW], a[VW];
     ld<VW>(p.x + e * VW, xv);
     ld<VW>(p.dy + e * VW, dv);
-    ld<VW>(p.mean + c0, mu);
-    ld<VW>(p.invstd + c0, is);
-    ld<VW>(p.gamma + c0, ga);
-    ld<VW>(p.beta + c0, be);
-    ld<VW>(p.k12 + c0, k1);
-    ld<VW>(p.k12 + p.C + c0, k2);
 #pragma unroll
     for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
     if (p.gate || p.addn) {
+      const long r = (long)p.dCV.div((uint32_t)e);
       const long img = (long)p.dHW.div((uint32_t)r);
       if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
       if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
@@ -417,6 +425,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
 }
 
 static unsigned ew_grid(long nv) { return std::min<unsigned>(std::max(cdiv(nv, 256), 1u), 8192); }
+
+// ew_grid with 256 * grid a multiple of cv when the grid-stride loop iterates (see bn_apply_kernel)
+static unsigned ew_grid_c(long nv, int cv) {
+  unsigned g = ew_grid(nv);
+  if ((long)g * 256 >= nv) return g;  // one element per thread
+  int a = 256, b = cv;
+  while (b) { const int t = a % b; a = b; b = t; }
+  const unsigned m = (unsigned)(cv / a);  // 256 * g % cv == 0  <=>  g % m == 0
+  return std::max(m, g / m * m);
+}
 
 static size_t red_ws_doubles(long rows, int C) {
   int nbx, rpb;
@@ -518,9 +536,9 @@ static int bn_apply_impl(const float* x, int64_t rows, int c, const float* mean,
   PLD_CHECK_ARG(rows * c < (1L << 31), "elementwise: tensor too large");
   hipStream_t st = as_stream(stream);
   if (c % 4 == 0) {
-    bn_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(p);
+    bn_apply_kernel<4><<<ew_grid_c(rows * c / 4, c / 4), 256, 0, st>>>(p);
   } else {
-    bn_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(p);
+    bn_apply_kernel<1><<<ew_grid_c(rows * c, c), 256, 0, st>>>(p);
   }
   return check_launch("bn_apply_kernel");
 }
@@ -554,9 +572,9 @@ extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const
   PLD_CHECK_ARG(rows * c < (1L << 31), "elementwise: tensor too large");
   hipStream_t st = as_stream(stream);
   if (c % 4 == 0) {
-    bn_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(p);
+    bn_apply_kernel<4><<<ew_grid_c(rows * c / 4, c / 4), 256, 0, st>>>(p);
   } else {
-    bn_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(p);
+    bn_apply_kernel<1><<<ew_grid_c(rows * c, c), 256, 0, st>>>(p);
   }
   return check_launch("bn_apply_kernel(affine)");
 }
@@ -617,9 +635,9 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
   q.dres = dres;
   q.dres_acc = dres_accumulate;
   if (c % 4 == 0) {
-    bn_bwd_apply_kernel<4><<<ew_grid(rows * c / 4), 256, 0, st>>>(q);
+    bn_bwd_apply_kernel<4><<<ew_grid_c(rows * c / 4, c / 4), 256, 0, st>>>(q);
   } else {
-    bn_bwd_apply_kernel<1><<<ew_grid(rows * c), 256, 0, st>>>(q);
+    bn_bwd_apply_kernel<1><<<ew_grid_c(rows * c, c), 256, 0, st>>>(q);
   }
   return check_launch("bn_bwd_apply_kernel");
 }

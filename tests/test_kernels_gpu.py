@@ -249,7 +249,10 @@ def test_channel_sum(cuda):
 
 # ------------------------------------------------------------------------------------ BN
 @pytest.mark.parametrize("rows,c,act", [(4096, 32, "relu"), (999, 144, "swish"),
-                                        (300, 1280, "swish"), (50, 6, "none")])
+                                        (300, 1280, "swish"), (50, 6, "none"),
+                                        # grid-stride apply loops (> 8192 x 256 vectors): the
+                                        # grid is a multiple of C / VW groups per thread
+                                        (100003, 96, "swish"), (2100007, 3, "relu")])
 def test_bn_forward_backward(cuda, rows, c, act):
     torch.manual_seed(rows + c)
     x = torch.randn(rows, c, dtype=torch.float64) * 3 + 1.5
