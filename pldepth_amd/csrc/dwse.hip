@@ -195,8 +195,9 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __res
   }
 }
 
-// input gradient, any stride: one output pixel per thread, taps of matching parity only
-template <int K>
+// input gradient, stride S (compile-time: the tap parity test and the divide are a mask and a
+// shift for S = 2): one output pixel per thread, taps of matching parity only
+template <int K, int S>
 __global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restrict__ dy,
                                                            const float* __restrict__ wt,
                                                            DwGeom g, float* __restrict__ dx,
@@ -215,14 +216,14 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restri
 #pragma unroll
     for (int ty = 0; ty < K; ++ty) {
       const int ny = iy + g.pt - ty;
-      if (ny < 0 || ny % g.s) continue;
-      const int oy = ny / g.s;
+      if (ny < 0 || ny % S) continue;
+      const int oy = ny / S;
       if (oy >= g.oh) continue;
 #pragma unroll
       for (int tx = 0; tx < K; ++tx) {
         const int nx = ix + g.pl - tx;
-        if (nx < 0 || nx % g.s) continue;
-        const int ox = nx / g.s;
+        if (nx < 0 || nx % S) continue;
+        const int ox = nx / S;
         if (ox >= g.ow) continue;
         const float4 v = *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c);
         const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
@@ -558,6 +559,7 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
   PLD_CHECK_ARG((long)n * h * w * c < (1L << 31) && (long)n * oh * ow * c < (1L << 31),
                 "pld_dwconv_dgrad: tensor too large for 32-bit indexing");
   PLD_CHECK_ARG(k == 3 || k == 5, "pld_dwconv_dgrad: kernel size %d unsupported (3, 5)", k);
+  PLD_CHECK_ARG(s == 1 || s == 2, "pld_dwconv_dgrad: stride %d unsupported (1, 2)", s);
   DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
   g.dRows = FastDiv((uint32_t)h);
   hipStream_t st = as_stream(stream);
@@ -574,8 +576,8 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
   } else {
     g.dTiles = FastDiv((uint32_t)w);
     const long total = (long)n * h * w * (c / 4);
-    if (k == 3) dwconv_dgrad_kernel<3><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
-    else dwconv_dgrad_kernel<5><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    if (k == 3) dwconv_dgrad_kernel<3, 2><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    else dwconv_dgrad_kernel<5, 2><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
   }
   return check_launch("dwconv_dgrad_kernel");
 }

@@ -52,6 +52,87 @@ struct UpPro {
   int act;
 };
 
+// 2x bilinear upsample, one thread per INPUT cell (i, j) and channel quad: the four outputs
+// (2i + a, 2j + b) read only rows i-1..i+1 / columns j-1..j+1 (clamped), so the 3x3 cells are
+// loaded (and BN-prologued) once for four outputs instead of 4 taps per output; every output is
+// still formed by lerp_coords' taps and the same top/bottom arithmetic (bit-identical).
+template <bool PRO>
+__global__ __launch_bounds__(256) void upsample2x_fwd_cell_kernel(
+    const float* __restrict__ x, int n, int h, int w, int c, UpPro pr, float* __restrict__ y,
+    FastDiv dCV, FastDiv dW, FastDiv dH) {
+  const uint32_t total = (uint32_t)n * dH.d * dW.d * dCV.d;
+  const int W2 = 2 * w;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    const uint32_t t = dCV.div(e);
+    const int q = (int)(e - t * dCV.d);
+    const uint32_t t2 = dW.div(t);
+    const int j = (int)(t - t2 * dW.d);
+    const uint32_t img_u = dH.div(t2);
+    const int i = (int)(t2 - img_u * dH.d);
+    const float* base = x + (long)img_u * h * w * c + q * 4;
+    float4 mu, is, ga, be;
+    if (PRO) {
+      mu = *reinterpret_cast<const float4*>(pr.mean + q * 4);
+      is = *reinterpret_cast<const float4*>(pr.invstd + q * 4);
+      ga = *reinterpret_cast<const float4*>(pr.gamma + q * 4);
+      be = *reinterpret_cast<const float4*>(pr.beta + q * 4);
+    }
+    // cells[r][s] = input (rr[r], cc[s]) with rr = {i-1, i, i+1} clamped (same for columns)
+    const int rr[3] = {max(i - 1, 0), i, min(i + 1, h - 1)};
+    const int cc[3] = {max(j - 1, 0), j, min(j + 1, w - 1)};
+    float4 cell[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        float4 v = *reinterpret_cast<const float4*>(base + ((long)rr[r] * w + cc[s2]) * c);
+        if (PRO) {
+          v.x = act_fwd(pr.act, ((v.x - mu.x) * is.x) * ga.x + be.x);
+          v.y = act_fwd(pr.act, ((v.y - mu.y) * is.y) * ga.y + be.y);
+          v.z = act_fwd(pr.act, ((v.z - mu.z) * is.z) * ga.z + be.z);
+          v.w = act_fwd(pr.act, ((v.w - mu.w) * is.w) * ga.w + be.w);
+        }
+        cell[r][s2] = v;
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      int y0, y1;
+      float yl;
+      lerp_coords(2 * i + a, h, y0, y1, yl);
+      // y0 / y1 as an index into rr: y0 is i-1 (clamped) or i, y1 is i or i+1 (clamped)
+      const int r0 = a == 0 ? 0 : 1, r1 = a == 0 ? 1 : 2;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        int x0, x1;
+        float xl;
+        lerp_coords(2 * j + b, w, x0, x1, xl);
+        const int s0 = b == 0 ? 0 : 1, s1 = b == 0 ? 1 : 2;
+        const float4 tl = cell[r0][s0], tr = cell[r0][s1], bl = cell[r1][s0], br = cell[r1][s1];
+        float4 o;
+        {
+          const float top = tl.x + (tr.x - tl.x) * xl, bot = bl.x + (br.x - bl.x) * xl;
+          o.x = top + (bot - top) * yl;
+        }
+        {
+          const float top = tl.y + (tr.y - tl.y) * xl, bot = bl.y + (br.y - bl.y) * xl;
+          o.y = top + (bot - top) * yl;
+        }
+        {
+          const float top = tl.z + (tr.z - tl.z) * xl, bot = bl.z + (br.z - bl.z) * xl;
+          o.z = top + (bot - top) * yl;
+        }
+        {
+          const float top = tl.w + (tr.w - tl.w) * xl, bot = bl.w + (br.w - bl.w) * xl;
+          o.w = top + (bot - top) * yl;
+        }
+        *reinterpret_cast<float4*>(y + (((long)img_u * 2 * h + 2 * i + a) * W2 + 2 * j + b) * c +
+                                   q * 4) = o;
+      }
+    }
+  }
+}
+
 template <int VW, bool PRO>
 __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const float* __restrict__ x, int n,
                                                              int h, int w, int c, UpPro pr,
@@ -240,8 +321,9 @@ extern "C" int pld_upsample2x_fwd_bn(const float* x, int n, int h, int w, int c,
   const FastDiv dW2((uint32_t)(2 * w)), dH2((uint32_t)(2 * h));
   if (c % 4 == 0) {
     const FastDiv dCV((uint32_t)(c / 4));
-    if (mean) upsample2x_fwd_kernel<4, true><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
-    else upsample2x_fwd_kernel<4, false><<<grid_for(total / 4), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
+    const FastDiv dW((uint32_t)w), dH((uint32_t)h);
+    if (mean) upsample2x_fwd_cell_kernel<true><<<grid_for(total / 16), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW, dH);
+    else upsample2x_fwd_cell_kernel<false><<<grid_for(total / 16), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW, dH);
   } else {
     const FastDiv dCV((uint32_t)c);
     if (mean) upsample2x_fwd_kernel<1, true><<<grid_for(total), 256, 0, st>>>(x, n, h, w, c, pr, y, dCV, dW2, dH2);
