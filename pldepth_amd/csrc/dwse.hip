@@ -195,47 +195,76 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __res
   }
 }
 
-// input gradient, stride S (compile-time: the tap parity test and the divide are a mask and a
-// shift for S = 2): one output pixel per thread, taps of matching parity only
-template <int K, int S>
-__global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const float* __restrict__ dy,
-                                                           const float* __restrict__ wt,
-                                                           DwGeom g, float* __restrict__ dx,
-                                                           int accum) {
+// input gradient, stride 2, one thread per 2x2 block of dx pixels (2a + u, 2b + v). With the pad
+// parities PTP = pt & 1, PLP = pl & 1 fixed at compile time, the taps of output (u, v) are the
+// (ty, tx) with ty = u + PTP and tx = v + PLP (mod 2) — every tap serves exactly one of the four
+// outputs — and dy row (2a + u + pt - ty) / 2 = a + pt / 2 + (u + PTP - ty) / 2: a window of
+// (K + 3) / 2 dy rows x columns at compile-time offsets, each loaded once (the per-pixel kernel
+// re-read it for every output). Each output sums its taps in ascending (ty, tx) order.
+template <int K, int PTP, int PLP>
+__global__ __launch_bounds__(256) void dwconv_dgrad_s2_kernel(const float* __restrict__ dy,
+                                                              const float* __restrict__ wt,
+                                                              DwGeom g, float* __restrict__ dx,
+                                                              int accum) {
+  constexpr int DMIN = -(K - 1) / 2;  // (u + PTP - ty) / 2 ranges over [DMIN, 1]
+  constexpr int NW = 2 - DMIN;
   const int cv = g.c / 4;
-  const int total = g.n * g.h * g.w * cv;
+  const int bw = (g.w + 1) / 2, bh = (g.h + 1) / 2;
+  const int total = g.n * bh * bw * cv;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int t0 = (int)g.dCV.div((uint32_t)e);
     const int q = e - t0 * cv;
-    const int t1 = (int)g.dTiles.div((uint32_t)t0);  // tiles == w here
-    const int ix = t0 - t1 * g.w;
-    const int img = (int)g.dRows.div((uint32_t)t1);
-    const int iy = t1 - img * g.h;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int t1 = (int)g.dTiles.div((uint32_t)t0);  // tiles == bw
+    const int b = t0 - t1 * bw;
+    const int img = (int)g.dRows.div((uint32_t)t1);  // rows == bh
+    const int a = t1 - img * bh;
     const float* db = dy + (long)img * g.oh * g.ow * g.c + 4 * q;
+    const int oy0 = a + (g.pt >> 1) + DMIN, ox0 = b + (g.pl >> 1) + DMIN;
+    float4 win[NW][NW];
+#pragma unroll
+    for (int r = 0; r < NW; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < NW; ++s2) {
+        const int oy = oy0 + r, ox = ox0 + s2;
+        win[r][s2] = ((unsigned)oy < (unsigned)g.oh && (unsigned)ox < (unsigned)g.ow)
+                         ? *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    float4 acc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) acc[u][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* wq = wt + 4 * q;
 #pragma unroll
     for (int ty = 0; ty < K; ++ty) {
-      const int ny = iy + g.pt - ty;
-      if (ny < 0 || ny % S) continue;
-      const int oy = ny / S;
-      if (oy >= g.oh) continue;
+      const int u = (ty + PTP) & 1;  // ty = u + PTP (mod 2)
+      const int r = (u + PTP - ty) / 2 - DMIN;
 #pragma unroll
       for (int tx = 0; tx < K; ++tx) {
-        const int nx = ix + g.pl - tx;
-        if (nx < 0 || nx % S) continue;
-        const int ox = nx / S;
-        if (ox >= g.ow) continue;
-        const float4 v = *reinterpret_cast<const float4*>(db + ((long)oy * g.ow + ox) * g.c);
-        const float4 f = *reinterpret_cast<const float4*>(wt + (ty * K + tx) * g.c + 4 * q);
-        acc = fma4(acc, v, f);
+        const int v = (tx + PLP) & 1;
+        const int s2 = (v + PLP - tx) / 2 - DMIN;
+        const float4 f = *reinterpret_cast<const float4*>(wq + (ty * K + tx) * g.c);
+        acc[u][v] = fma4(acc[u][v], win[r][s2], f);
       }
     }
-    float4* d = reinterpret_cast<float4*>(dx + (long)e * 4);
-    if (accum) {
-      const float4 o = *d;
-      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int iy = 2 * a + u;
+      if (iy >= g.h) break;
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int ix = 2 * b + v;
+        if (ix >= g.w) continue;
+        float4* d = reinterpret_cast<float4*>(dx + (((long)img * g.h + iy) * g.w + ix) * g.c + 4 * q);
+        float4 o = acc[u][v];
+        if (accum) {
+          const float4 old = *d;
+          o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+        }
+        *d = o;
+      }
     }
-    *d = acc;
   }
 }
 
@@ -574,10 +603,18 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
     else
       dwconv_dgrad_s1_kernel<5, T, R><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
   } else {
-    g.dTiles = FastDiv((uint32_t)w);
-    const long total = (long)n * h * w * (c / 4);
-    if (k == 3) dwconv_dgrad_kernel<3, 2><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
-    else dwconv_dgrad_kernel<5, 2><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    const int bw = (w + 1) / 2, bh = (h + 1) / 2;
+    g.dTiles = FastDiv((uint32_t)bw);
+    g.dRows = FastDiv((uint32_t)bh);
+    const unsigned grid = grid_for((long)n * bh * bw * (c / 4));
+    const int par = (pad_t & 1) * 2 + (pad_l & 1);
+#define PLD_DWS2(KK)                                                                              \
+  if (par == 0) dwconv_dgrad_s2_kernel<KK, 0, 0><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
+  else if (par == 1) dwconv_dgrad_s2_kernel<KK, 0, 1><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
+  else if (par == 2) dwconv_dgrad_s2_kernel<KK, 1, 0><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
+  else dwconv_dgrad_s2_kernel<KK, 1, 1><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    if (k == 3) { PLD_DWS2(3) } else { PLD_DWS2(5) }
+#undef PLD_DWS2
   }
   return check_launch("dwconv_dgrad_kernel");
 }

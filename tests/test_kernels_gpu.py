@@ -416,6 +416,31 @@ def test_dwconv(cuda, n, h, w, c, k, s):
     assert rel_err(dx, x.grad) < 1e-5
 
 
+@pytest.mark.parametrize("k", [3, 5])
+@pytest.mark.parametrize("pt,pl", [(0, 0), (0, 1), (1, 0), (1, 1), (2, 1), (2, 2)])
+@pytest.mark.parametrize("h,w", [(9, 11), (10, 7)])
+def test_dwconv_dgrad_stride2_every_pad_parity(cuda, k, pt, pl, h, w):
+    """The 2x2-block stride-2 dgrad (one kernel per pad parity) against autograd, odd and even
+    sizes (ragged last block row / column), with accumulate."""
+    if pt >= k or pl >= k:
+        pytest.skip("pad >= kernel")
+    n, c = 2, 8
+    torch.manual_seed(k * 100 + pt * 10 + pl)
+    x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
+    wk = torch.randn(k, k, c, dtype=torch.float64)
+    oh, ow = (h + pt - k) // 2 + 1, (w + pl - k) // 2 + 1
+    pb = max(0, (oh - 1) * 2 + k - h - pt)
+    pr = max(0, (ow - 1) * 2 + k - w - pl)
+    y_ref = OE.dwconv(x.permute(0, 3, 1, 2), wk, 2, (pt, pb, pl, pr)).permute(0, 2, 3, 1)
+    assert y_ref.shape[1:3] == (oh, ow)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    dx = torch.full((n, h, w, c), 0.5, device=cuda)
+    K.dwconv_dgrad(dev(dy, cuda), dev(wk, cuda), k, 2, pt, pl, dx, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(dx - 0.5, x.grad) < 1e-5, rel_err(dx - 0.5, x.grad)
+
+
 @pytest.mark.parametrize("k,s", [(3, 1), (5, 2), (5, 1), (3, 2)])
 def test_dwconv_fused_bn_swish(cuda, k, s):
     """pld_dwconv_fwd_bn == dwconv(swish(bn(x))) with batch statistics; padding taps read 0
