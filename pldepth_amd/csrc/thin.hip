@@ -89,7 +89,9 @@ template <int KR>
 static void thin_launch(const float* a, const float* b, const float* bias, float* out, int M,
                         int N, int acc, hipStream_t st) {
   const unsigned grid = (unsigned)cdiv(M, 64);
-  if (N % 16 == 0 && N >= 128) thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
+  // CH = 16 only when the chunks split evenly over the 4 waves (N = 144: 18 chunks of 8 balance
+  // 5/5/4/4, 9 chunks of 16 would leave three waves idle a third of the time)
+  if (N % 64 == 0 && N >= 128) thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
   else thin1x1_kernel<KR, 8><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
 }
 
