@@ -210,24 +210,43 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const float* __rest
     const uint32_t img_u = dH.div(t2);
     const int ky = (int)(t2 - img_u * dH.d);
     const int img = (int)img_u;
+    // the 4 x 4 adjoint window at fixed positions (rows 2k-1 .. 2k+2): an absent edge tap gets
+    // weight 0 and a clamped (valid) address, so all 16 loads are unconditional and in flight
+    // together; fma(0, v, r) = r keeps every sum equal to adj_taps' present-taps-only order
+    const int H2 = 2 * h;
     int oy[4], ox[4];
     float wy[4], wx[4];
-    const int ny = adj_taps(ky, h, oy, wy);
-    const int nx = adj_taps(kx, w, ox, wx);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      oy[a] = min(max(2 * ky - 1 + a, 0), H2 - 1);
+      ox[a] = min(max(2 * kx - 1 + a, 0), W2 - 1);
+    }
+    wy[0] = ky >= 1 ? 0.25f : 0.f;
+    wy[1] = ky == 0 ? 1.0f : 0.75f;
+    wy[2] = ky == h - 1 ? 1.0f : 0.75f;
+    wy[3] = ky <= h - 2 ? 0.25f : 0.f;
+    wx[0] = kx >= 1 ? 0.25f : 0.f;
+    wx[1] = kx == 0 ? 1.0f : 0.75f;
+    wx[2] = kx == w - 1 ? 1.0f : 0.75f;
+    wx[3] = kx <= w - 2 ? 0.25f : 0.f;
     const float* base = dy + (long)img * 2 * h * W2 * c + q * VW;
+    float v[4][4][VW];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ld4<VW>(base + ((long)oy[a] * W2 + ox[b]) * c, v[a][b]);
     float s[VW];
 #pragma unroll
     for (int u = 0; u < VW; ++u) s[u] = 0.f;
-    for (int a = 0; a < ny; ++a) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
       float rs[VW];
 #pragma unroll
       for (int u = 0; u < VW; ++u) rs[u] = 0.f;
-      for (int b = 0; b < nx; ++b) {
-        float v[VW];
-        ld4<VW>(base + ((long)oy[a] * W2 + ox[b]) * c, v);
 #pragma unroll
-        for (int u = 0; u < VW; ++u) rs[u] += wx[b] * v[u];
-      }
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int u = 0; u < VW; ++u) rs[u] += wx[b] * v[a][b][u];
 #pragma unroll
       for (int u = 0; u < VW; ++u) s[u] += wy[a] * rs[u];
     }
