@@ -48,8 +48,11 @@ def synthetic_batch(B, H, W, seed):
 
 
 def profile_conv(trainer, lr):
-    """One eager step with HIP events around every conv launch (on the stream the kernels run
-    on). Returns {kernel family (pld_conv_kernel_kind): [algorithmic FLOPs, seconds, launches]}."""
+    """One eager step with HIP events around every conv call (on the stream the kernels run on).
+    Returns one record per call: (kernel name, family kind, mode, algorithmic FLOPs, algorithmic
+    HBM bytes, seconds). The kernel name is the main kernel the call launched
+    (pld_conv_kernel_name: the name rocprof lists); a call's time includes the split-K slab
+    reduction it may add."""
     import ctypes
     from pldepth_amd import kernels as K
     from pldepth_amd._lib import lib
@@ -62,6 +65,12 @@ def profile_conv(trainer, lr):
         # fwd, dX and dW of one conv are the same contraction: 2 * outputs * taps * Cin * Cout
         return 2.0 * a.n * a.oh * a.ow * a.cout * a.kh * a.kw * (a.c1 + a.c2)
 
+    def bytes_of(a):
+        # the two activations the contraction reads / writes (input x | dX, output y | dY) and
+        # the filter (w | dW), each once: 4 B per element
+        return 4.0 * (a.n * a.h * a.w * (a.c1 + a.c2) + a.n * a.oh * a.ow * a.cout
+                      + a.kh * a.kw * (a.c1 + a.c2) * a.cout)
+
     def wrap(name):
         fn = orig[name]
 
@@ -73,8 +82,9 @@ def profile_conv(trainer, lr):
             saved = args.tile  # classify by the schedule the call actually ran
             args.tile = getattr(args, "_used_tile", saved)
             kind = lib().pld_conv_kernel_kind(ctypes.byref(args), mode_of[name])
+            kname = lib().pld_conv_kernel_name(ctypes.byref(args), mode_of[name]).decode()
             args.tile = saved
-            recs.append((kind, flops_of(args), e0, e1))
+            recs.append((kname, kind, mode_of[name], flops_of(args), bytes_of(args), e0, e1))
             return r
         return w
 
@@ -86,40 +96,68 @@ def profile_conv(trainer, lr):
     finally:
         for n, f in orig.items():
             setattr(K, n, f)
-    out = {}
-    for kind, fl, e0, e1 in recs:
-        d = out.setdefault(kind, [0.0, 0.0, 0])
+    return [(n, k, m, f, b, e0.elapsed_time(e1) / 1e3) for n, k, m, f, b, e0, e1 in recs]
+
+
+def conv_roofline(recs, traffic_profile=None):
+    """roofline object. Top level = the DOMINANT kernel (the conv kernel name with the largest
+    summed time in the profiled step): achieved = its algorithmic FLOPs / its measured time, peak
+    = the MFMA peak of its arithmetic. `family` keeps the whole conv family (FLOP-weighted blend
+    of the families' peaks: the same FLOPs with every launch at its own family's peak). traffic
+    (PMC HBM bytes) cannot be read inside this process: null here; the PMC pass of the same
+    command is committed under profiles/ (traffic_profile) with the algorithmic bytes beside it."""
+    fam, by_name = {}, {}
+    for name, kind, mode, fl, by, sec in recs:
+        d = fam.setdefault(kind, [0.0, 0.0, 0])
         d[0] += fl
-        d[1] += e0.elapsed_time(e1) / 1e3
+        d[1] += sec
         d[2] += 1
-    return out
-
-
-def conv_roofline(prof, traffic_file):
-    """roofline object of the conv family. achieved = algorithmic FLOPs / measured time; peak =
-    the FLOP-weighted harmonic mean of the families' peaks (the same FLOPs, each family at its
-    own peak); traffic = HBM bytes per launch from the committed PMC summary when present."""
-    fl = sum(v[0] for v in prof.values())
-    sec = sum(v[1] for v in prof.values())
-    n = sum(v[2] for v in prof.values())
-    t_peak = sum(v[0] / (KIND_PEAK[k] * 1e12) for k, v in prof.items())
-    achieved = fl / sec / 1e12
-    peak = fl / t_peak / 1e12
-    traffic = None
-    if traffic_file and os.path.exists(traffic_file):
-        with open(traffic_file) as f:
-            traffic = json.load(f).get("conv_bytes_per_launch")
+        e = by_name.setdefault(name, {"kind": kind, "flops": 0.0, "bytes": 0.0, "sec": 0.0,
+                                      "launches": 0, "modes": set()})
+        e["flops"] += fl
+        e["bytes"] += by
+        e["sec"] += sec
+        e["launches"] += 1
+        e["modes"].add(("fwd", "dgrad", "wgrad")[mode])
+    fl = sum(v[0] for v in fam.values())
+    sec = sum(v[1] for v in fam.values())
+    t_peak = sum(v[0] / (KIND_PEAK[k] * 1e12) for k, v in fam.items())
+    dname = max(by_name, key=lambda n: by_name[n]["sec"])
+    d = by_name[dname]
+    d_ach = d["flops"] / d["sec"] / 1e12
+    d_peak = KIND_PEAK[d["kind"]]
+    dominant = {
+        "kernel": dname, "family": KIND_NAME[d["kind"]], "modes": sorted(d["modes"]),
+        "launches_per_step": d["launches"], "flops_per_step": d["flops"],
+        "bytes_per_step": d["bytes"], "avg_us": round(d["sec"] / d["launches"] * 1e6, 2),
+        "ms_per_step": round(d["sec"] * 1e3, 4), "achieved_tflops": round(d_ach, 3),
+        "peak_tflops": round(d_peak, 1), "frac": round(d_ach / d_peak, 4),
+        "achieved_gbps": round(d["bytes"] / d["sec"] / 1e9, 1),
+    }
     return {
         "bound": "mfma",
-        "kernel": "conv family: conv_x3_kernel / conv_x3_patch* (bf16x3 MFMA) + "
-                  "conv_igemm_kernel (fp32 MFMA) + direct VALU kernels (Cout=1 3x3, thin 1x1); fwd/dgrad/wgrad",
-        "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "TFLOP/s",
-        "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
-        "flops_per_step": fl,
-        "families": {KIND_NAME[k]: {"tflop": round(v[0] / 1e12, 4), "ms": round(v[1] * 1e3, 3),
-                                    "launches": v[2], "achieved": round(v[0] / v[1] / 1e12, 2),
-                                    "peak": round(KIND_PEAK[k], 1)}
-                     for k, v in sorted(prof.items())},
+        "kernel": dname,
+        "achieved": round(d_ach, 3), "peak": round(d_peak, 1), "unit": "TFLOP/s",
+        "frac": round(d_ach / d_peak, 4),
+        "traffic": None,
+        "traffic_profile": traffic_profile,
+        "dominant": dominant,
+        "family": {
+            "kernel": "conv family: conv_x3_kernel / conv_x3_patch* (bf16x3 MFMA) + "
+                      "conv_igemm_kernel (fp32 MFMA) + direct VALU kernels (Cout=1 3x3, thin 1x1)",
+            "achieved": round(fl / sec / 1e12, 3), "peak": round(fl / t_peak / 1e12, 3),
+            "frac": round((fl / sec) / (fl / t_peak), 4), "launches": sum(v[2] for v in
+                                                                          fam.values()),
+            "flops_per_step": fl, "ms_per_step": round(sec * 1e3, 3),
+            "families": {KIND_NAME[k]: {"tflop": round(v[0] / 1e12, 4),
+                                        "ms": round(v[1] * 1e3, 3), "launches": v[2],
+                                        "achieved": round(v[0] / v[1] / 1e12, 2),
+                                        "peak": round(KIND_PEAK[k], 1)}
+                         for k, v in sorted(fam.items())},
+        },
+        "kernels": {n: {"ms": round(v["sec"] * 1e3, 3), "launches": v["launches"],
+                        "achieved_tflops": round(v["flops"] / v["sec"] / 1e12, 2)}
+                    for n, v in sorted(by_name.items(), key=lambda kv: -kv[1]["sec"])},
     }
 
 
@@ -177,7 +215,9 @@ def cpu_baseline(H, W, L, R, model="ff_effnet", seconds_budget=25.0):
         one_step(n_steps + 2)
         t_total += time.perf_counter() - t0
         n_steps += 1
-    return {"value": B * n_steps / t_total, "unit": "images/s", "cores": 8, "kind": "port",
+    return {"value": B * n_steps / t_total, "unit": "images/s",
+            "cores": len(os.sched_getaffinity(0)), "threads": torch.get_num_threads(),
+            "kind": "port",
             "sample": f"{n_steps} timed full train steps after 1 warm-up (numpy Info sampler + "
                       f"torch-CPU fp32 {model} fwd/bwd + ListMLE + Adam-AMSGrad), batch {B}, "
                       f"{H}x{W}, L={L}, R={R}, torch.set_num_threads(8)"}
@@ -207,6 +247,56 @@ def _cpu_weights(H, W):
     return e.get_weights()
 
 
+def run_config(model, H, B, L, R, sampling_type, steps, warmup, rank, world, pg, graph=True):
+    """Build a replica for one workload, warm it up (the first step is eager: it tunes conv
+    schedules and sizes workspaces, then the step is captured), time `steps` graph replays
+    bracketed by barrier + synchronize. Returns (trainer, seconds)."""
+    from pldepth_amd.trainer import ReplicaTrainer
+    tr = ReplicaTrainer((H, H, 3), B, L, R, sampling_type, seed=0, rank=rank,
+                        world_size=world, process_group=pg, model=model)
+    x, gt, mask = synthetic_batch(B, H, H, seed=1000 + rank)
+    if model == "ff_redweb":
+        x = tr.engine.preprocess(x)  # the data pipeline's caffe preprocessing (PLDepth.py:169)
+    tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
+                 torch.from_numpy(mask).cuda())
+    lr = 0.01
+    tr.step_eager(lr)
+    torch.cuda.synchronize()
+    if graph:
+        tr.capture()
+    for _ in range(max(warmup - 1, 0)):
+        tr.step(lr)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(lr)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return tr, elapsed
+
+
+# BASELINE.json configs measured beside the headline (1 GPU): (key, model, L, R)
+EXTRA_CONFIGS = [
+    ("cfg3_ff_resnet", "ff_redweb", 5, 100),
+    ("cfg5_ff_effnet_L64_R1000", "ff_effnet", 64, 1000),
+]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,12 +311,14 @@ def main():
                     help="ff_redweb = the ResNet-50 backbone (BASELINE cfg3 'ff_resnet')")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the cfg3 (ff_resnet) and cfg5 (L=64, R=1000) lines (1 GPU only)")
     ap.add_argument("--conv-math", default="auto", choices=["auto", "mixed", "bf16x3", "fp32"],
                     help="conv arithmetic policy (kernels.conv_policy): auto = decoder bf16x3, "
                          "encoder bf16x3 where the BN sees >= 4096 values per channel (all of "
                          "them at 448x448 batch 32); mixed = encoder fp32, decoder bf16x3")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "conv_traffic.json"),
-                    help="PMC traffic summary of the conv family (tools/traffic.py --json)")
+    ap.add_argument("--traffic-profile", default="profiles/r02_pmc_dominant.txt",
+                    help="committed PMC summary of the dominant kernel (named in the line)")
     ap.add_argument("--tile-cache", default="",
                     help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
@@ -246,59 +338,24 @@ def main():
     from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
     from pldepth_amd import kernels as K
     K.set_conv_math(a.conv_math)
-    from pldepth_amd.trainer import ReplicaTrainer
-
-    H = W = a.size
-    B, L, R = a.batch, a.ranking_size, a.rankings_per_image
-    tr = ReplicaTrainer((H, W, 3), B, L, R, a.sampling_type, seed=0, rank=rank,
-                        world_size=world, process_group=pg, model=a.model)
-    x, gt, mask = synthetic_batch(B, H, W, seed=1000 + rank)
-    if a.model == "ff_redweb":
-        x = tr.engine.preprocess(x)  # the data pipeline's caffe preprocessing (PLDepth.py:169)
-    tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
-                 torch.from_numpy(mask).cuda())
-    lr = 0.01
-    from pldepth_amd import kernels as K
     if a.tile_cache and os.path.exists(a.tile_cache):
         K.load_tile_cache(a.tile_cache)
-    # first step eager: tunes conv schedules, sizes every workspace, then capture the graph(s)
-    tr.step_eager(lr)
-    torch.cuda.synchronize()
+
+    H = a.size
+    B, L, R = a.batch, a.ranking_size, a.rankings_per_image
+    tr, elapsed = run_config(a.model, H, B, L, R, a.sampling_type, a.steps, a.warmup, rank,
+                             world, pg, graph=not a.no_graph)
     if a.tile_cache and rank == 0:
         K.save_tile_cache(a.tile_cache)
-    if not a.no_graph:
-        tr.capture()
-    for _ in range(max(a.warmup - 1, 0)):
-        tr.step(lr)
-    torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        tr.step(lr)
-    tr.synchronize()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     loss = tr.loss_value()
     value = world * B * a.steps / elapsed
 
-    # conv family: algorithmic FLOPs / measured duration (HIP events, eager step)
-    prof = profile_conv(tr, lr)
+    # dominant conv kernel + conv family: algorithmic FLOPs / measured duration (HIP events on
+    # the trainer's stream, one eager step)
+    recs = profile_conv(tr, 0.01)
     flops_img = tr.engine.conv_flops_per_image()
-    roof = conv_roofline(prof, a.traffic_file)
-    roof["step_frac"] = round(value / world * flops_img / 1e12 / roof["peak"], 4)
+    roof = conv_roofline(recs, a.traffic_profile)
+    roof["step_frac"] = round(value / world * flops_img / 1e12 / roof["family"]["peak"], 4)
     out = {
         "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
         "value": round(value, 3),
@@ -310,13 +367,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32 (bf16x3 MFMA)",
         "data": "synthetic (U[0,1) RGB, smooth 8-bit depth, Bernoulli(0.9) mask; Keras-default "
                 "random-init weights)",
-        "config": {"workload": f"{a.model} train step {H}x{W}, per-GPU batch {B}, "
+        "config": {"workload": f"{a.model} train step {H}x{H}, per-GPU batch {B}, "
                                f"ranking_size {L}, rankings_per_image {R}, "
                                f"sampler {tr.strategy}, Adam-AMSGrad",
-                   "model": a.model, "global_batch": world * B, "input": f"{H}x{W}",
+                   "model": a.model, "global_batch": world * B, "input": f"{H}x{H}",
                    "ranking_size": L, "rankings_per_image": R,
                    "parallelism": f"dp{world}", "graph": not a.no_graph},
         "conv_math": {"policy": a.conv_math, "encoder": tr.engine.enc_math,
@@ -324,8 +381,22 @@ def main():
         "roofline": roof,
         "loss": loss,
     }
+    del tr
+    if world == 1 and not a.no_extra_configs and a.model == "ff_effnet" and H == 448:
+        extra = {}
+        for key, model, el, er in EXTRA_CONFIGS:
+            t2, el_s = run_config(model, H, B, el, er, a.sampling_type, a.steps, a.warmup,
+                                  rank, world, pg, graph=not a.no_graph)
+            extra[key] = {"value": round(B * a.steps / el_s, 3), "unit": "images/s",
+                          "ms_per_step": round(1e3 * el_s / a.steps, 3), "model": model,
+                          "input": f"{H}x{H}", "batch": B, "ranking_size": el,
+                          "rankings_per_image": er, "sampler": t2.strategy,
+                          "loss": t2.loss_value()}
+            del t2
+            torch.cuda.empty_cache()
+        out["extra_configs"] = extra
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(H, W, L, R, a.model)
+        out["cpu_baseline"] = cpu_baseline(H, H, L, R, a.model)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

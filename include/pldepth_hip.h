@@ -138,6 +138,10 @@ int pld_conv_schedule_class(int math, int idx);
  * accounting (each family has its own peak). */
 enum { PLD_KIND_FP32 = 0, PLD_KIND_BF16X3 = 1, PLD_KIND_DIRECT = 2 };
 int pld_conv_kernel_kind(const pld_conv_args* a, int mode);
+/* the name of the main kernel that call launches ("conv_x3_kernel", "conv_x3_patch_wgrad_kernel",
+ * "conv_igemm_kernel", "thin1x1_kernel", "skinny_fwd_kernel", ...; "" on bad arguments): lets a
+ * caller attribute HIP-event timings to rocprof kernel names (bench.py roofline.dominant). */
+const char* pld_conv_kernel_name(const pld_conv_args* a, int mode);
 size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a);
 size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a);
 

@@ -83,7 +83,8 @@ class JSONLLogger(object):
 @click.option('--input_size', default=224, type=click.INT)
 @click.option('--data_npz', default='', help='npz with imgs/gts/masks arrays')
 @click.option('--hr_wsi_path', default='', help='HR-WSI root ({train,val}/{imgs,gts,valid_masks})')
-@click.option('--save_path', default='', help='save weights (.npz) after training')
+@click.option('--save_path', default='', help='save weights after training (.h5: Keras HDF5, '
+              'else .npz) and the whole model as <stem>_model.h5')
 @click.option('--log_jsonl', default='', help='per-batch metrics file')
 def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_size,
                                rankings_per_image, initial_lr, equality_threshold,
@@ -116,17 +117,25 @@ def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_siz
     shape = [input_size, input_size, 3]
     model, preprocess_fn = get_pl_depth_net(model_params, shape)
 
-    if hr_wsi_path:  # PLDepth.py:100-110: HR-WSI train split, decoded + resized (dao/hr_wsi.py)
+    # eval split for the test pass (PLDepth.py:151,184-192: HR-WSI 'val', first 250 images)
+    eval_imgs = eval_gts = None
+    if hr_wsi_path:  # PLDepth.py:139-151: HR-WSI train split, decoded + resized (dao/hr_wsi.py)
         from .data.dao.hr_wsi import HRWSITFDataAccessObject
         dao = HRWSITFDataAccessObject(hr_wsi_path, shape, seed)
         imgs, gts, masks = dao.get_training_dataset(size=ds_size)
         gts = gts[..., 0]
+        eval_imgs, eval_gts, _ = dao.get_validation_dataset()
+        eval_imgs, eval_gts = eval_imgs[:250], eval_gts[:250, ..., 0]
     elif data_npz:
         with np.load(data_npz, allow_pickle=False) as z:
             imgs, gts, masks = z["imgs"], z["gts"], z["masks"]
+            if "val_imgs" in z.files:
+                eval_imgs, eval_gts = z["val_imgs"][:250], z["val_gts"][:250]
     else:
         imgs, gts, masks = synthetic_hrwsi(ds_size or 8 * batch_size, input_size, input_size,
                                            seed)
+        n_eval = min(250, max(batch_size, len(imgs) // 15))
+        eval_imgs, eval_gts, _ = synthetic_hrwsi(n_eval, input_size, input_size, seed + 1)
     ds_size = len(imgs)
     n_val = ds_size // 15
     steps_per_epoch = max(1, int((ds_size * 14 / 15) / batch_size))  # PLDepth.py:120
@@ -143,14 +152,24 @@ def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_siz
     val_ds = (provider.provide_val_dataset(preprocess_fn(imgs[:n_val]), gts[:n_val])
               if n_val >= batch_size else None)
     callbacks = [TerminateOnNaN(), schedule, LearningRateLoggingCallback(), JSONLLogger(log_jsonl)]
+    if model_checkpoints:  # tracking_utils.py:21-30 (best val_loss -> Keras .h5 model file)
+        from .util.env import get_config
+        from .util.tracking_utils import construct_model_checkpoint_callback
+        callbacks.append(construct_model_checkpoint_callback(get_config(), model_name, 1))
     model.fit(x=train_ds, epochs=epochs, steps_per_epoch=steps_per_epoch, callbacks=callbacks,
               validation_data=val_ds, verbose=1)
-    if save_path:
+    if save_path:  # PLDepth.py:180-181: weights, plus the whole model as .h5
         model.save_weights(save_path)
-    # test pass (PLDepth.py:183-192): ordinal error and nDCG@200 on up to 250 held-out images,
-    # on the GPU (pldepth_amd.active_learning.metrics); the reference's pair / list draws need
-    # >= 10,000 and >= 224*224 pixels per image
-    test_img, test_gt = preprocess_fn(imgs[:n_val][:250]), gts[:n_val][:250]
+        model.save(save_path.rsplit(".", 1)[0] + "_model.h5")
+    # test pass (PLDepth.py:183-192): ordinal error and nDCG@200 on the first 250 images of the
+    # held-out eval split, on the GPU (pldepth_amd.active_learning.metrics). Like the reference,
+    # the images go in raw (no preprocess_fn: PLDepth.py:187-191 calls calc_err / dcg_metric on
+    # the DAO's [0,1] images; for ff_effnet preprocessing is the identity anyway). The
+    # reference's pair / list draws need >= 10,000 and >= 224*224 pixels per image.
+    if eval_imgs is None:
+        print("no eval split (--data_npz without val_imgs/val_gts): test pass skipped")
+        return 0
+    test_img, test_gt = eval_imgs, eval_gts
     if len(test_img) and input_size * input_size >= 2 * 5000:
         err = calc_err(model, test_img, test_gt[..., None], img_size=(input_size, input_size))
         print(f"test_error {err:.6f}")

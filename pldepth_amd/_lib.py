@@ -53,6 +53,7 @@ _SIGS = {
     "pld_conv_num_schedules": (I32, [I32]),
     "pld_conv_schedule_class": (I32, [I32, I32]),
     "pld_conv_kernel_kind": (I32, [C.POINTER(ConvArgs), I32]),
+    "pld_conv_kernel_name": (C.c_char_p, [C.POINTER(ConvArgs), I32]),
     "pld_conv2d_fwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_dgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_filter_to_native": (I32, [P, I32, I32, I32, I32, P, P]),
@@ -105,7 +106,7 @@ _SIGS = {
 # functions returning a value rather than a status
 _NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_num_schedules",
                "pld_conv_schedule_class",
-               "pld_conv_kernel_kind",
+               "pld_conv_kernel_kind", "pld_conv_kernel_name",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",

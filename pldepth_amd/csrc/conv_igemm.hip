@@ -974,6 +974,34 @@ extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
   return x3 ? PLD_KIND_BF16X3 : PLD_KIND_FP32;
 }
 
+// the name of the main kernel a conv call launches (for per-kernel roofline accounting and for
+// matching HIP-event timings with rocprof's kernel names); "" on bad arguments. Split-K slab
+// reductions a call may add are not named (they are part of the call's time).
+static bool wgrad_patch_geom(const pld_conv_args* a);
+extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
+  const int kind = pld_conv_kernel_kind(a, mode);
+  if (kind < 0) return "";
+  if (kind == PLD_KIND_DIRECT) {
+    if (pld__skinny_eligible(a))
+      return mode == 0 ? "skinny_fwd_kernel" : mode == 1 ? "skinny_dgrad_kernel"
+                                                         : "skinny_wgrad_kernel";
+    return "thin1x1_kernel";
+  }
+  if (kind == PLD_KIND_FP32) return "conv_igemm_kernel";
+  if (pld_conv_schedule_class(a->math, a->tile) != PLD_SCHED_X3_PATCH) return "conv_x3_kernel";
+  const int cfg = a->tile - 2 * pld__x3_num_cfg();
+  if (mode == 2) return wgrad_patch_geom(a) ? "conv_x3_patch_wgrad_kernel" : "conv_x3_kernel";
+  // FWD view (dgrad: the input is dY, cout channels, one source)
+  const int c1 = mode == 0 ? a->c1 : a->cout, c2 = mode == 0 ? a->c2 : 0;
+  const bool geo = a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 &&
+                   a->in_scale == nullptr && a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 &&
+                   a->pad_l <= 2;
+  if (!geo) return "conv_x3_kernel";
+  if (c1 == 32 && c2 == 0) return "conv_x3_patch_kernel";
+  return (cfg == 0 && c1 % 16 == 0 && c2 % 16 == 0) ? "conv_x3_patch_mc_kernel"
+                                                      : "conv_x3_kernel";
+}
+
 extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
   if (pld__skinny_eligible(a)) return 0;

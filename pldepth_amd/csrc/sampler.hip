@@ -223,8 +223,13 @@ __global__ __launch_bounds__(256) void candidate_kernel(RankParams p) {
     float g[LMAX];
     int id[LMAX];
     for (int j = 0; j < L; ++j) {
+      if (nv <= 0) {  // empty mask: nothing was compacted; a defined, all-invalid list (label
+        id[j] = 0;    // -1: ListMLE's validity mask), never a read of the unwritten valid_idx
+        g[j] = -1.0f;
+        continue;
+      }
       int d = dr[j];
-      d = min(max(d, 0), max(nv - 1, 0));
+      d = min(max(d, 0), nv - 1);
       const int pos = vi[d];
       id[j] = pos;
       g[j] = gb[pos];
@@ -297,10 +302,14 @@ __global__ __launch_bounds__(256) void candidate_wave_kernel(RankParams p) {
     int id = 0;
     if (lane < L) {
       const int nv = p.nvalid[b];
-      int d = p.draws[e * L + lane];
-      d = min(max(d, 0), max(nv - 1, 0));
-      id = p.valid_idx[(long)b * HW + d];
-      g = p.gt[(long)b * HW + id];
+      if (nv > 0) {
+        int d = p.draws[e * L + lane];
+        d = min(max(d, 0), nv - 1);
+        id = p.valid_idx[(long)b * HW + d];
+        g = p.gt[(long)b * HW + id];
+      } else {  // empty mask: defined all-invalid list (see candidate_kernel)
+        g = -1.0f;
+      }
     }
     int rank = 0;
     for (int k = 0; k < L; ++k) {  // wave-uniform trip count: every lane takes part in the shfl

@@ -33,6 +33,10 @@ def _f32(t):
 
 
 _ws_cache = {}
+# workspaces superseded while a captured hipGraph exists: the graph holds their raw pointers,
+# so they stay allocated (never returned to the caching allocator) until every graph is gone
+_ws_retired = []
+_LIVE_GRAPHS = [0]
 
 
 def workspace(nbytes, key="default"):
@@ -41,6 +45,8 @@ def workspace(nbytes, key="default"):
     k = (dev, key)
     buf = _ws_cache.get(k)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None and _LIVE_GRAPHS[0] > 0:
+            _ws_retired.append(buf)
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device="cuda")
         _ws_cache[k] = buf
     return buf
@@ -88,6 +94,7 @@ class Graph:
     def capture(self, fn):
         lib().pld_graph_begin(stream())
         _CAPTURING[0] = True
+        _LIVE_GRAPHS[0] += 1
         try:
             fn()
         finally:
@@ -106,6 +113,10 @@ class Graph:
                 lib().pld_graph_destroy(self.exec)
             except Exception:
                 pass
+            self.exec = None
+            _LIVE_GRAPHS[0] -= 1
+            if _LIVE_GRAPHS[0] == 0:
+                _ws_retired.clear()
 
 
 # ------------------------------------------------------------------------------------ conv
@@ -199,18 +210,45 @@ _TILE_CACHE = {}
 _CAPTURING = [False]
 
 
+def _tile_cache_meta():
+    """What a tuned schedule index means depends on the schedule tables of THIS library build
+    and on the GPU: a cache from another build / arch is ignored."""
+    import hashlib
+    from ._lib import LIB_PATH
+    h = hashlib.sha1()
+    with open(LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName \
+        if torch.cuda.is_available() else "none"
+    return {"lib_sha1": h.hexdigest(), "arch": arch,
+            "num_schedules": [lib().pld_conv_num_schedules(m) for m in sorted(MATH.values())]}
+
+
 def load_tile_cache(path):
-    """Merge schedules tuned by an earlier run (JSON written by save_tile_cache)."""
+    """Merge schedules tuned by an earlier run (JSON written by save_tile_cache). Returns the
+    number of entries taken: 0 when the file was written by another library build or for
+    another GPU arch, and entries whose index is out of range are dropped."""
     import json
     with open(path) as f:
-        for k, v in json.load(f):
-            _TILE_CACHE[tuple(k)] = int(v)
+        d = json.load(f)
+    if not isinstance(d, dict) or d.get("meta") != _tile_cache_meta():
+        return 0
+    n_sched = dict(zip(sorted(MATH.values()), d["meta"]["num_schedules"]))
+    taken = 0
+    for k, v in d.get("entries", []):
+        k, v = tuple(k), int(v)
+        if -1 <= v < n_sched.get(k[-1], 0):
+            _TILE_CACHE[k] = v
+            taken += 1
+    return taken
 
 
 def save_tile_cache(path):
     import json
     with open(path, "w") as f:
-        json.dump([[list(k), v] for k, v in _TILE_CACHE.items()], f)
+        json.dump({"meta": _tile_cache_meta(),
+                   "entries": [[list(k), v] for k, v in _TILE_CACHE.items()]}, f)
 
 
 def _shape_key(mode, a):

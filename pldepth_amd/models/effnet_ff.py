@@ -82,6 +82,14 @@ def same_pad(size, k, s):
 class EffNetFF:
     """Keras-named parameters + buffers + launch order of one ff_effnet replica."""
 
+    # Keras' automatic names of the decoder layers pl_hourglass.py:59-96 leaves unnamed (a fresh
+    # session), for the .h5 import/export (util/keras_h5.py)
+    KERAS_RENAME = dict([(f"dec_conv{i}", "conv2d" + (f"_{i}" if i else "")) for i in range(6)]
+                        + [(f"dec_bn{i}", "batch_normalization" + (f"_{i}" if i else ""))
+                           for i in range(5)])
+    # the Normalization layer's adapt() counter, which Keras saves with its mean / variance
+    KERAS_EXTRA_WEIGHTS = {"normalization": [("count", np.array(0, np.int64))]}
+
     def __init__(self, input_shape=(448, 448, 3), batch_size=32, device="cuda", seed=0,
                  conv_math=None):
         H, W, C = input_shape

@@ -1,9 +1,13 @@
 """Building blocks shared by the HIP model engines (ff_effnet, ff_redweb): flat parameter
 stores and Keras-named BatchNormalization / Conv2D wrappers around libpldepth_hip.so."""
+import itertools
+
 import numpy as np
 import torch
 
 from .. import kernels as K
+
+_SEQ = itertools.count()  # creation order of stored tensors across an engine's stores
 
 BN_EPS = 1e-3        # keras BatchNormalization defaults
 BN_MOMENTUM = 0.99
@@ -14,6 +18,7 @@ class FlatStore:
 
     def __init__(self):
         self.specs = []  # (name, shape, offset)
+        self.order = {}  # name -> global creation index (graph order: keras_layout)
         self.size = 0
         self.buf = None
         self.views = {}
@@ -21,6 +26,7 @@ class FlatStore:
     def add(self, name, shape):
         n = int(np.prod(shape))
         self.specs.append((name, tuple(shape), self.size))
+        self.order[name] = next(_SEQ)
         self.size += (n + 3) // 4 * 4
         return name
 
@@ -33,7 +39,7 @@ class FlatStore:
 
     def like(self):
         t = FlatStore()
-        t.specs, t.size = self.specs, self.size
+        t.specs, t.size, t.order = self.specs, self.size, self.order
         return t
 
     def __getitem__(self, name):

@@ -68,6 +68,11 @@ class FullyFledgedModel(object):
                                       beta_1=self.optimizer.beta_1, beta_2=self.optimizer.beta_2,
                                       epsilon=self.optimizer.epsilon)
         self._captured = False
+        pending = getattr(self, "_pending_optimizer_state", None)
+        if pending:  # a load_model()ed file: restore its Adam slots now that they exist
+            from ..util import keras_h5
+            keras_h5.load_optimizer_state(self, pending)
+            self._pending_optimizer_state = None
 
     def train_on_batch(self, x, y, return_loss=True):
         """One optimizer step on (x [B,H,W,3], y [B,R,L,2]); returns the batch loss (float)."""
@@ -198,7 +203,14 @@ class FullyFledgedModel(object):
         self.engine.set_weights(weights)
 
     def save_weights(self, path):
-        """Keras-named float32 arrays (HWIO kernels) in an .npz archive (+ optimizer slots)."""
+        """``.h5`` / ``.hdf5`` / ``.keras``: the Keras HDF5 weights format (util/keras_h5.py;
+        what the reference's load_weights reads, PLDepth.py:136-137). Any other path: an .npz of
+        Keras-named float32 arrays (HWIO kernels) plus the Adam slots, for exact resume (the
+        reference writes a TF checkpoint there, a format this build does not implement)."""
+        if path.endswith((".h5", ".hdf5", ".keras")):
+            from ..util import keras_h5
+            keras_h5.save_weights(self.engine, path)
+            return
         w = self.get_weights()
         if self.trainer is not None:
             m, v, vh = self.engine.adam_state()
@@ -208,6 +220,11 @@ class FullyFledgedModel(object):
         np.savez(path if path.endswith(".npz") else path + ".npz", **w)
 
     def load_weights(self, path):
+        """Keras HDF5 (weights or whole-model file; detected by signature) or this build's .npz."""
+        from ..util import hdf5
+        if hdf5.is_hdf5(path):
+            from ..util import keras_h5
+            return keras_h5.load_weights(self.engine, path)
         path = path if path.endswith(".npz") else path + ".npz"
         with np.load(path, allow_pickle=False) as z:
             w = {k: z[k] for k in z.files}
@@ -217,6 +234,21 @@ class FullyFledgedModel(object):
             for store, name in ((m, "m"), (v, "v"), (vh, "vhat")):
                 store.copy_(torch.from_numpy(w[f"__adam__/{name}"]))
             self.trainer.step_dev.copy_(torch.from_numpy(w["__adam__/step"]))
+
+    def save(self, filepath, overwrite=True, include_optimizer=True, **kwargs):
+        """keras.Model.save('... .h5') (PLDepth.py:181): model config, weights and the Adam
+        slots in Keras' HDF5 model layout; ``load_model`` (models/__init__.py) reads it back."""
+        import os
+        from ..util import keras_h5
+        if not overwrite and os.path.exists(filepath):
+            raise FileExistsError(filepath)
+        opt = self.optimizer
+        if not include_optimizer:
+            self.optimizer = None
+        try:
+            keras_h5.save_model(self, filepath)
+        finally:
+            self.optimizer = opt
 
     def count_params(self):
         return self.engine.count_trainable()

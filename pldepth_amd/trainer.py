@@ -76,15 +76,29 @@ class ReplicaTrainer:
         """images [B,H,W,3] model input (the [0,1] images after the model's preprocess_fn:
         identity for ff_effnet, caffe mean subtraction for ff_redweb), gt [B,H,W], mask [B,H,W]
         (>0 valid) — host or device.
-        The copies are ordered on the trainer's stream (before the next step's kernels)."""
+        The copies are ordered on the trainer's stream (before the next step's kernels), after
+        whatever the caller's current stream has queued (e.g. the sampler or a producer kernel
+        that wrote a device source)."""
+        self._order_after_caller()
         with torch.cuda.stream(self.stream):
-            if images is not None:
-                self.x.copy_(torch.as_tensor(images, dtype=torch.float32).reshape(self.x.shape))
-            if gt is not None:
-                self.gt.copy_(torch.as_tensor(gt, dtype=torch.float32).reshape(self.gt.shape))
-            if mask is not None:
-                self.mask.copy_(torch.as_tensor(mask, dtype=torch.float32)
-                                .reshape(self.mask.shape))
+            for src, dst in ((images, self.x), (gt, self.gt), (mask, self.mask)):
+                if src is not None:
+                    t = torch.as_tensor(src, dtype=torch.float32)
+                    dst.copy_(t.reshape(dst.shape))
+                    self._keep_alive(t)
+
+    def _order_after_caller(self):
+        """The trainer's stream waits for the caller's current stream: device tensors handed
+        to set_batch / set_rankings may still be in flight there."""
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)
+
+    def _keep_alive(self, t):
+        """A device source freed by the caller must not be recycled before the trainer stream's
+        copy has read it (caching-allocator reuse across streams)."""
+        if t.is_cuda:
+            t.record_stream(self.stream)
 
     def set_rankings(self, y_true):
         """External rankings [B, R, L, 2] (float32 flat index, depth) for the next step."""
@@ -96,8 +110,10 @@ class ReplicaTrainer:
             self.R_out = R
             self.y_true = torch.empty(self.B, R, self.L, 2, device=self.device)
             self.nll = torch.empty(self.B * R, device=self.device)
+        self._order_after_caller()
         with torch.cuda.stream(self.stream):
             self.y_true.copy_(y.reshape(self.y_true.shape))
+            self._keep_alive(y)
 
     # ------------------------------------------------------------------ phases
     def _sample(self):

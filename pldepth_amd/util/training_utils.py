@@ -97,3 +97,44 @@ class TerminateOnNaN(Callback):
         if loss is not None and not np.isfinite(loss):
             logging.warning("Batch %d: Invalid loss, terminating training", batch)
             self.model.stop_training = True
+
+
+class ModelCheckpoint(Callback):
+    """keras.callbacks.ModelCheckpoint as tracking_utils.py:21-30 builds it (monitor='val_loss',
+    save_best_only=True): at each epoch end, save the model (``model.save``: Keras HDF5 model
+    file, util/keras_h5.py) or only its weights, when ``monitor`` improved (mode 'auto': 'min'
+    unless the name contains 'acc'). ``filepath`` may hold ``{epoch}`` / log-key format fields."""
+
+    def __init__(self, filepath, monitor="val_loss", verbose=0, save_best_only=False,
+                 save_weights_only=False, mode="auto", save_freq="epoch", **kwargs):
+        super().__init__()
+        if save_freq != "epoch":
+            raise NotImplementedError("ModelCheckpoint: save_freq='epoch' only")
+        self.filepath, self.monitor, self.verbose = filepath, monitor, verbose
+        self.save_best_only, self.save_weights_only = save_best_only, save_weights_only
+        if mode == "auto":
+            mode = "max" if "acc" in monitor else "min"
+        self.better = np.less if mode == "min" else np.greater
+        self.best = np.inf if mode == "min" else -np.inf
+
+    def on_epoch_end(self, epoch, logs=None):
+        logs = logs or {}
+        path = self.filepath.format(epoch=epoch + 1, **logs)
+        if self.save_best_only:
+            cur = logs.get(self.monitor)
+            if cur is None:
+                logging.warning("ModelCheckpoint: %s not available, skipping", self.monitor)
+                return
+            if not self.better(cur, self.best):
+                if self.verbose:
+                    logging.info("Epoch %d: %s did not improve from %.5f", epoch + 1,
+                                 self.monitor, self.best)
+                return
+            if self.verbose:
+                logging.info("Epoch %d: %s improved from %.5f to %.5f, saving model to %s",
+                             epoch + 1, self.monitor, self.best, cur, path)
+            self.best = cur
+        if self.save_weights_only:
+            self.model.save_weights(path)
+        else:
+            self.model.save(path)

@@ -102,6 +102,29 @@ def test_fit_predict_save_load(cuda, tmp_path):
     model2.compile(loss=HourglassNegativeLogLikelihood(L, B), optimizer=Adam(0.01, amsgrad=True))
     model2.load_weights(path)
     np.testing.assert_array_equal(model2.predict(imgs[:3]), p1)
+    # Keras HDF5: weights file (load_weights, PLDepth.py:136-137) and whole-model file with the
+    # Adam slots (model.save, :181 -> load_model, run_scripts/rnd_on_info_pretrain.py:98)
+    h5w = str(tmp_path / "w.h5")
+    model.save_weights(h5w)
+    model3, _ = get_pl_depth_net(mp, [H, H, 3])
+    assert model3.load_weights(h5w) == "name"
+    np.testing.assert_array_equal(model3.predict(imgs[:3]), p1)
+    h5m = str(tmp_path / "m.h5")
+    model.save(h5m)
+    from pldepth_amd.models import load_model
+    model4 = load_model(h5m)
+    model4.compile(loss=HourglassNegativeLogLikelihood(L, B), optimizer=Adam(0.01, amsgrad=True))
+    np.testing.assert_array_equal(model4.predict(imgs[:3]), p1)
+    for a, b in zip(model.engine.adam_state(), model4.engine.adam_state()):
+        assert torch.equal(a, b)
+    assert int(model4.trainer.step_dev.item()) == int(model.trainer.step_dev.item())
+    # one more identical step on both: resume is exact
+    xb, yb = next(iter(train))
+    model4.optimizer.lr = model.optimizer.lr
+    model.train_on_batch(xb, yb)
+    model4.train_on_batch(xb, yb)
+    np.testing.assert_array_equal(model.get_weights()["dec_conv2/kernel"],
+                                  model4.get_weights()["dec_conv2/kernel"])
 
 
 def test_redweb_factory_fit_predict(cuda):

@@ -1,0 +1,340 @@
+"""Parity at the benchmark's own configurations and arithmetic (BASELINE.json configs).
+
+* cfg2 arithmetic: ff_effnet at 448x448 with bf16x3 convs everywhere (what the bench times at
+  batch 32) — every trainable gradient against the fp64 oracle, next to the fp32 restatement's
+  own error on the same input.
+* drop-connect (on in every timed step): HIP keep scales bit-exact vs the Philox restatement
+  (oracle/philox.py), keep rate and 1/(1-rate) scale, forward + gradients with those scales
+  injected into the oracle (oracle/effnet.py forward(drop_scales=...)).
+* cfg1: one whole ReplicaTrainer step (GPU sampler -> fwd -> ListMLE -> bwd -> Adam-AMSGrad) at
+  224x224, B=2, L=2, R=100 against the oracle chain (sampler bit-exact, loss, gradients, update).
+* cfg3: ff_redweb (ResNet-50 + ReDWeb) at 448x448 against oracle/redweb.py.
+* cfg5: the full-size ListMLE (B=32, R=1000, L=64: 2,048,000 list elements, heavy duplicate
+  pixels) against oracle/listmle.py.
+
+Gradient bar (BASELINE.json: 1e-3 relative): wherever the fp32 restatement of the reference
+semantics itself lands within 1e-3 of fp64, the HIP gradient must too; where it does not (BN
+over few pixels and ReLU masks make single tensors ill-conditioned at test batch sizes), the HIP
+gradient must be no further from fp64 than 2x the fp32 restatement. Reports of every tensor are
+written to $PLD_REPORT_DIR when set.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import effnet as OE
+from oracle import listmle as LM
+from oracle import philox as PX
+from oracle import redweb as OR
+from oracle import sampler as S
+from oracle.adam import adam_amsgrad_step
+from pldepth_amd import kernels as K
+from pldepth_amd.models.effnet_ff import EffNetFF
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+def make_rankings(rng, B, H, W, R, L):
+    idx = rng.integers(0, H * W, (B, R, L))
+    lab = rng.permutation(B * R * L).reshape(B, R, L) / (B * R * L)
+    lab = -np.sort(-lab, axis=-1)
+    return np.ascontiguousarray(np.stack([idx.astype(np.float32), lab.astype(np.float32)], -1))
+
+
+def report(name, obj):
+    d = os.environ.get("PLD_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"parity_{name}.json"), "w") as f:
+            json.dump(obj, f, indent=1)
+
+
+def effnet_structural_zero(name):
+    """exact-arithmetic zeros (tests/test_model_gpu.py::_structural_zero)"""
+    return ((name.startswith("dec_conv") and name.endswith("/bias"))
+            or name.endswith("project_bn/beta"))
+
+
+def check_gradients(tag, hip, g64, g32, structural_zero):
+    """The bar of the module docstring; returns the per-tensor report."""
+    keys = [k for k in g64 if not structural_zero(k)]
+    rows, fails = {}, []
+    for k in keys:
+        e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64[k])
+        bar = TOL if e32 <= TOL else 2.0 * e32
+        rows[k] = {"hip": e_hip, "fp32_restatement": e32, "bar": bar}
+        if e_hip > bar:
+            fails.append((k, e_hip, e32))
+    flat = lambda g: torch.cat([torch.as_tensor(g[k]).detach().double().cpu().flatten()
+                                for k in keys])
+    a, b, c = flat(hip), flat(g64), flat(g32)
+    glob = {"hip_rel_l2": float((a - b).norm() / b.norm()),
+            "fp32_rel_l2": float((c - b).norm() / b.norm()),
+            "cos": float(a @ b / (a.norm() * b.norm())),
+            "tensors": len(keys),
+            "tensors_fp32_within_1e-3": sum(r["fp32_restatement"] <= TOL for r in rows.values()),
+            "tensors_hip_within_1e-3": sum(r["hip"] <= TOL for r in rows.values())}
+    scale = float(b.abs().max())
+    for k in g64:
+        if structural_zero(k):
+            assert float(torch.as_tensor(hip[k]).abs().max()) <= 1e-3 * scale + 1e-6, k
+    report(tag, {"global": glob, "tensors": rows})
+    print(f"[{tag}] {glob}")
+    assert not fails, fails[:10]
+    assert glob["hip_rel_l2"] <= max(TOL, 2.0 * glob["fp32_rel_l2"])
+    return glob
+
+
+# ------------------------------------------------------------ cfg2 arithmetic at 448x448
+def test_effnet_448_bf16x3_gradients(cuda):
+    B, H, R, L = 2, 448, 100, 5
+    eng = EffNetFF((H, H, 3), B, seed=0, conv_math="bf16x3")
+    eng.drop_connect = False
+    rng = np.random.default_rng(5)
+    x = rng.random((B, H, H, 3)).astype(np.float32)
+    weights = eng.get_weights()
+    eng.act["input"].copy_(torch.from_numpy(x))
+    pred = eng.forward(training=True)
+    y = make_rankings(rng, B, H, H, R, L)
+    loss, dpred, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
+    eng.backward(dpred)
+    torch.cuda.synchronize()
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    x64 = torch.tensor(x, dtype=torch.float64)
+    with torch.no_grad():
+        pred_ref = OE.forward(P, x64)
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
+    assert rel(pred, pred_ref) < TOL
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < TOL
+    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref))
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float())
+    hip = {k: eng.grads[k] for k in g64}
+    glob = check_gradients("effnet448_bf16x3", hip, g64, g32, effnet_structural_zero)
+    assert glob["cos"] > 0.9999
+
+
+# ------------------------------------------------------------------- drop-connect
+def _residual_drop_blocks(eng):
+    return [(li, blk) for li, blk in enumerate(eng.blocks) if blk["residual"] and blk["rate"] > 0]
+
+
+@pytest.mark.parametrize("rate", [0.0125, 0.1875, 0.5])
+def test_dropconnect_scales_bit_exact_and_keep_rate(cuda, rate):
+    n, seed = 8192, 11
+    out = torch.empty(n, device=cuda)
+    zeros = 0
+    for step in range(1, 9):
+        K.dropconnect_scales(out, rate, seed, step, layer=7, image_offset=3)
+        got = out.cpu().numpy()
+        ref = PX.dropconnect_scales(n, rate, seed, step, layer=7, image_offset=3)
+        np.testing.assert_array_equal(got, ref)
+        zeros += int((got == 0).sum())
+        # graph-replayable form (device step counter) is the same stream
+        K.dropconnect_scales(out, rate, seed, torch.tensor([step], dtype=torch.int64,
+                                                           device=cuda), layer=7, image_offset=3)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    keep = got[got != 0]
+    assert np.all(keep == np.float32(1) / (np.float32(1) - np.float32(rate)))
+    N = 8 * n
+    assert abs(zeros / N - rate) < 5 * np.sqrt(rate * (1 - rate) / N)
+
+
+def test_sampler_draws_bit_exact_vs_philox(cuda):
+    nv = np.array([1, 7, 1000, 200704], np.int32)
+    d = torch.empty(4, 500, 5, dtype=torch.int32, device=cuda)
+    K.sampler_draw(torch.from_numpy(nv).to(cuda), 500, 5, seed=1234, step=(1 << 33) + 7,
+                   image_offset=5, draws=d)
+    np.testing.assert_array_equal(d.cpu().numpy(),
+                                  PX.sampler_draws(nv, 500, 5, 1234, (1 << 33) + 7, 5))
+
+
+def test_dropconnect_forward_and_gradients(cuda):
+    """Drop-connect as the timed step runs it: the per-block (step, image)-keyed scales read
+    back from the engine and injected into the oracle."""
+    B, H, R, L, seed = 4, 128, 24, 5, 0
+    eng = EffNetFF((H, H, 3), B, seed=seed, conv_math="fp32")
+    eng.drop_connect = True
+    blocks = _residual_drop_blocks(eng)
+    # a step whose masks drop at least one residual branch (the 1/(1-rate) scale alone is
+    # exercised by every kept one)
+    step = next(s for s in range(1, 200) if any(
+        (PX.dropconnect_scales(B, blk["rate"], seed, s, li) == 0).any() for li, blk in blocks))
+    rng = np.random.default_rng(2)
+    x = rng.random((B, H, H, 3)).astype(np.float32)
+    weights = eng.get_weights()
+    eng.act["input"].copy_(torch.from_numpy(x))
+    pred = eng.forward(training=True, step=step)
+    y = make_rankings(rng, B, H, H, R, L)
+    loss, dpred, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
+    eng.backward(dpred)
+    torch.cuda.synchronize()
+    drop = {}
+    for li, blk in blocks:
+        got = blk["drop"].cpu().numpy()
+        np.testing.assert_array_equal(got, PX.dropconnect_scales(B, blk["rate"], seed, step, li))
+        drop[blk["name"]] = torch.tensor(got, dtype=torch.float64)
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    x64 = torch.tensor(x, dtype=torch.float64)
+    taps = {}
+    with torch.no_grad():
+        pred_ref = OE.forward(P, x64, drop_scales=drop, taps=taps)
+        pred_nodrop = OE.forward(P, x64)
+    assert rel(pred_ref, pred_nodrop) > 1e-2  # the masks matter for this input
+    for name in ["block2b_output", "block5c_output", "block6d_output", "top_activation"]:
+        assert rel(eng.act[name], taps[name].permute(0, 2, 3, 1)) < TOL, name
+    assert rel(pred, pred_ref) < TOL
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < TOL
+    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
+                                 drop_scales={k: v.float() for k, v in drop.items()})
+    check_gradients("dropconnect128", {k: eng.grads[k] for k in g64}, g64, g32,
+                    effnet_structural_zero)
+
+
+# ------------------------------------------------------------------- cfg1: whole step
+def test_cfg1_trainer_step_224(cuda):
+    """BASELINE cfg1 (ff_effnet 224x224, B=2, L=2, R=100, Info sampler): one eager
+    ReplicaTrainer step — GPU sampler, forward with drop-connect, ListMLE, backward, Adam —
+    against the oracle chain fed the same Philox draws and drop scales."""
+    from pldepth_amd.trainer import ReplicaTrainer
+    B, H, L, R, lr = 2, 224, 2, 100, 0.01
+    tr = ReplicaTrainer((H, H, 3), B, L, R, 1, seed=0)
+    eng = tr.engine
+    rng = np.random.default_rng(9)
+    x = rng.random((B, H, H, 3)).astype(np.float32)
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, H), indexing="ij")
+    gt = np.stack([np.round(255 * (0.5 + 0.3 * np.sin((3 + b) * yy) * np.cos(2 * xx))) / 255
+                   for b in range(B)]).astype(np.float32)
+    mask = (rng.random((B, H, H)) < 0.9).astype(np.float32)
+    weights = eng.get_weights()
+    params0 = eng.params.buf.clone()
+    tr.set_batch(torch.from_numpy(x).to(cuda), torch.from_numpy(gt).to(cuda),
+                 torch.from_numpy(mask).to(cuda))
+    tr.step_eager(lr)
+    tr.synchronize()
+    # sampler: the step's Philox draws, then the reference's gather/sort/score/select, bit-exact
+    draws = tr.draws.cpu().numpy()
+    nv = [int((mask[b] > 0).sum()) for b in range(B)]
+    np.testing.assert_array_equal(draws, PX.sampler_draws(nv, draws.shape[1], L, 0, 1, 0))
+    y = tr.y_true.cpu().numpy()
+    for b in range(B):
+        ref, _ = S.sample_masked_point_batch("info", mask[b], gt[b], R, L, draws[b].reshape(-1))
+        np.testing.assert_array_equal(y[b], ref)
+    drop = {blk["name"]: torch.tensor(blk["drop"].cpu().numpy(), dtype=torch.float64)
+            for li, blk in _residual_drop_blocks(eng)}
+    for li, blk in _residual_drop_blocks(eng):
+        np.testing.assert_array_equal(drop[blk["name"]].numpy().astype(np.float32),
+                                      PX.dropconnect_scales(B, blk["rate"], 0, 1, li))
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    x64 = torch.tensor(x, dtype=torch.float64)
+    with torch.no_grad():
+        pred_ref = OE.forward(P, x64, drop_scales=drop)
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
+    assert abs(tr.loss_value() - loss_ref) / abs(loss_ref) < TOL
+    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
+                                 drop_scales={k: v.float() for k, v in drop.items()})
+    check_gradients("cfg1_224", {k: eng.grads[k] for k in g64}, g64, g32,
+                    effnet_structural_zero)
+    # Adam-AMSGrad (step 1) applied by the oracle to the step's own gradients
+    z = np.zeros(params0.numel(), np.float32)
+    p_ref, *_ = adam_amsgrad_step(params0.cpu().numpy(), eng.grads.buf.cpu().numpy(), z, z, z,
+                                  lr, 1)
+    np.testing.assert_allclose(eng.params.buf.cpu().numpy(), p_ref, rtol=1e-6, atol=1e-7)
+    assert int(tr.step_dev.item()) == 2
+
+
+# ------------------------------------------------------------------- cfg3: ff_redweb 448
+def test_cfg3_redweb_448(cuda):
+    from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input
+    B, H, R, L = 2, 448, 100, 5
+    eng = RedWebFF((H, H, 3), B, seed=0, conv_math="bf16x3")
+    rng = np.random.default_rng(4)
+    x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
+    weights = eng.get_weights()
+    eng.act["input"].copy_(torch.from_numpy(x))
+    pred = eng.forward(training=True)
+    y = make_rankings(rng, B, H, H, R, L)
+    loss, dpred, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
+    eng.backward(dpred)
+    torch.cuda.synchronize()
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    x64 = torch.tensor(x, dtype=torch.float64)
+    taps = {}
+    with torch.no_grad():
+        pred_ref = OR.forward(P, x64, taps=taps, preprocessed=True)
+    for name in ["conv1_relu", "conv2_block3_out", "conv3_block4_out", "conv4_block3_out",
+                 "conv5_block3_out", "ffl0", "ffl1"]:
+        mine = eng.act[name if not name.startswith("ffl") else name + "/out"]
+        assert rel(mine, taps[name].permute(0, 2, 3, 1)) < TOL, name
+    assert rel(pred, pred_ref) < TOL
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < TOL
+    assert rel(dpred, torch.tensor(dpred_ref)) < TOL
+    g64, _ = OR.train_step_grads(P, x64, torch.tensor(dpred_ref), preprocessed=True)
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    g32, _ = OR.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
+                                 preprocessed=True)
+    zeros = {"aol/conv0/bias", "aol/conv1/bias", "aol/conv2/bias"}
+    check_gradients("cfg3_redweb448_bf16x3", {k: eng.grads[k] for k in g64}, g64, g32,
+                    lambda k: k in zeros)
+
+
+# ------------------------------------------------------------------- cfg5: full ListMLE
+def test_cfg5_listmle_full_size(cuda):
+    """B=32, 448x448, R=1000, L=64: E = 2,048,000 gathered scores. Indices come from a pool of
+    20,000 pixels per image, so every pixel is hit ~100 times (duplicate-pixel scatter-add) and
+    lists hold repeated pixels as the sampler's with-replacement draws do."""
+    B, H, R, L = 32, 448, 1000, 64
+    rng = np.random.default_rng(64)
+    pred = (0.5 * rng.standard_normal((B, H, H, 1))).astype(np.float32)
+    pool = np.stack([rng.choice(H * H, 20000, replace=False) for _ in range(B)])
+    idx = np.take_along_axis(pool, rng.integers(0, 20000, (B, R * L)), 1).reshape(B, R, L)
+    lab = rng.random((B, R, L)).astype(np.float32)
+    lab = -np.sort(-lab, axis=-1)
+    y = np.ascontiguousarray(np.stack([idx.astype(np.float32), lab], -1))
+    loss_ref, dpred_ref = LM.hourglass_nll(y, pred, B, L)
+    loss, dpred, nll = K.listmle_fwd_bwd(torch.from_numpy(pred).to(cuda),
+                                         torch.from_numpy(y).to(cuda), B, R, L)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref) / abs(loss_ref) < 1e-5
+    assert rel(dpred, torch.from_numpy(dpred_ref)) < 1e-5
+    hit = np.zeros(B * H * H, bool)
+    hit[(idx + (np.arange(B) * H * H)[:, None, None]).reshape(-1)] = True
+    d = dpred.cpu().numpy().reshape(-1)
+    assert np.all(d[~hit] == 0)  # untouched pixels get exactly zero gradient
+
+
+# ------------------------------------------------------------------- empty masks
+def test_sampler_empty_mask_is_defined(cuda):
+    """an all-zero mask compacts nothing; the GPU path emits a defined all-invalid
+    list (index 0, label -1, masked by ListMLE) instead of reading unwritten memory, and the
+    per-image reference entry raises like np.random.randint(0) does (sampling.py:113)."""
+    from pldepth_amd.data.sampling import InformationScoreBasedSampling
+    from pldepth_amd.models.models_meta import ModelParameters
+    mp = ModelParameters()
+    mp.set_parameter("ranking_size", 5)
+    st = InformationScoreBasedSampling(mp)
+    H = 32
+    gt = torch.rand(2, H, H, device=cuda)
+    mask = torch.ones(2, H, H, device=cuda)
+    mask[1] = 0
+    out = st.sample_batch_gpu(gt, mask, 10, seed=1, step=1).cpu().numpy()
+    assert np.all(out[1, :, :, 0] == 0) and np.all(out[1, :, :, 1] == -1)
+    assert np.all(out[0, :, :, 1] >= 0)
+    with pytest.raises(ValueError):
+        st.sample_masked_point_batch(None, np.zeros((H, H)), np.ones((H, H)), 10)
