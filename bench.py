@@ -14,8 +14,11 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
+# before torch / the HIP runtime initialise: hipGraph replay correctness (pldepth_amd/__init__.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -114,9 +114,12 @@ class Graph:
             except Exception:
                 pass
             self.exec = None
-            _LIVE_GRAPHS[0] -= 1
-            if _LIVE_GRAPHS[0] == 0:
-                _ws_retired.clear()
+            try:
+                _LIVE_GRAPHS[0] -= 1
+                if _LIVE_GRAPHS[0] == 0:
+                    _ws_retired.clear()
+            except TypeError:  # interpreter shutdown: module globals already cleared
+                pass
 
 
 # ------------------------------------------------------------------------------------ conv

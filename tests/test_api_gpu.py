@@ -123,8 +123,9 @@ def test_fit_predict_save_load(cuda, tmp_path):
     model4.optimizer.lr = model.optimizer.lr
     model.train_on_batch(xb, yb)
     model4.train_on_batch(xb, yb)
-    np.testing.assert_array_equal(model.get_weights()["dec_conv2/kernel"],
-                                  model4.get_weights()["dec_conv2/kernel"])
+    # (equal up to the float-atomic summation order of ListMLE's duplicate-pixel scatter)
+    np.testing.assert_allclose(model.get_weights()["dec_conv2/kernel"],
+                               model4.get_weights()["dec_conv2/kernel"], rtol=1e-4, atol=1e-6)
 
 
 def test_redweb_factory_fit_predict(cuda):

@@ -59,10 +59,18 @@ def report(name, obj):
             json.dump(obj, f, indent=1)
 
 
-def effnet_structural_zero(name):
-    """exact-arithmetic zeros (tests/test_model_gpu.py::_structural_zero)"""
-    return ((name.startswith("dec_conv") and name.endswith("/bias"))
-            or name.endswith("project_bn/beta"))
+def effnet_structural_zero(name, dropped=()):
+    """exact-arithmetic zeros (tests/test_model_gpu.py::_structural_zero). A project_bn beta
+    stops being one when drop-connect scales its block's residual branch differently per image
+    (`dropped`: those block names): the constant then varies across the batch and survives the
+    next BN."""
+    if name.endswith("project_bn/beta"):
+        return name[:-len("project_bn/beta")] not in dropped
+    return name.startswith("dec_conv") and name.endswith("/bias")
+
+
+def _nonuniform(drop):
+    return {k for k, v in drop.items() if float(v.max()) != float(v.min())}
 
 
 def check_gradients(tag, hip, g64, g32, structural_zero):
@@ -200,8 +208,10 @@ def test_dropconnect_forward_and_gradients(cuda):
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
     g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
                                  drop_scales={k: v.float() for k, v in drop.items()})
+    nu = _nonuniform(drop)
+    assert nu  # at least one block's branch is scaled differently across the batch
     check_gradients("dropconnect128", {k: eng.grads[k] for k in g64}, g64, g32,
-                    effnet_structural_zero)
+                    lambda k: effnet_structural_zero(k, nu))
 
 
 # ------------------------------------------------------------------- cfg1: whole step
@@ -248,8 +258,9 @@ def test_cfg1_trainer_step_224(cuda):
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
     g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
                                  drop_scales={k: v.float() for k, v in drop.items()})
+    nu = _nonuniform(drop)
     check_gradients("cfg1_224", {k: eng.grads[k] for k in g64}, g64, g32,
-                    effnet_structural_zero)
+                    lambda k: effnet_structural_zero(k, nu))
     # Adam-AMSGrad (step 1) applied by the oracle to the step's own gradients
     z = np.zeros(params0.numel(), np.float32)
     p_ref, *_ = adam_amsgrad_step(params0.cpu().numpy(), eng.grads.buf.cpu().numpy(), z, z, z,
@@ -260,9 +271,13 @@ def test_cfg1_trainer_step_224(cuda):
 
 # ------------------------------------------------------------------- cfg3: ff_redweb 448
 def test_cfg3_redweb_448(cuda):
+    """The bench's 'auto' policy: decoder bf16x3; an encoder conv bf16x3 when its BN sees
+    >= 4096 values per channel (at the bench's batch 32 every ResNet stage does; at this test's
+    batch 2 the conv5 stage sees 14*14*2 = 392 and stays fp32 — bf16x3 there lands 1.2e-3 from
+    fp64 at conv5_block3_out, BN over few values amplifying the rounding)."""
     from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input
     B, H, R, L = 2, 448, 100, 5
-    eng = RedWebFF((H, H, 3), B, seed=0, conv_math="bf16x3")
+    eng = RedWebFF((H, H, 3), B, seed=0, conv_math="auto")
     rng = np.random.default_rng(4)
     x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
     weights = eng.get_weights()
@@ -290,7 +305,7 @@ def test_cfg3_redweb_448(cuda):
     g32, _ = OR.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
                                  preprocessed=True)
     zeros = {"aol/conv0/bias", "aol/conv1/bias", "aol/conv2/bias"}
-    check_gradients("cfg3_redweb448_bf16x3", {k: eng.grads[k] for k in g64}, g64, g32,
+    check_gradients("cfg3_redweb448_auto", {k: eng.grads[k] for k in g64}, g64, g32,
                     lambda k: k in zeros)
 
 
