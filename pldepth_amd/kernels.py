@@ -162,12 +162,13 @@ def conv_policy(policy=None):
     return (policy, policy)
 
 
-def encoder_math(enc_math, population):
+def encoder_math(enc_math, population, threshold=None):
     """Resolve an engine's encoder math for one conv whose BN sees `population` values per
-    channel (batch x output pixels)."""
+    channel (batch x output pixels); `threshold` defaults to X3_MIN_POPULATION (an engine may
+    carry its own: RedWebFF.x3_min_population)."""
     if enc_math != "auto":
         return enc_math
-    return "bf16x3" if population >= X3_MIN_POPULATION else "fp32"
+    return "bf16x3" if population >= (threshold or X3_MIN_POPULATION) else "fp32"
 
 
 def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None, in_shift=None,

@@ -235,7 +235,8 @@ class RedWebFF:
         if conv.trainable:
             return self.dec_math
         # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
-        return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1))
+        return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
+                              getattr(self, "x3_min_population", None))
 
     def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None):
         """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout]."""
@@ -255,7 +256,8 @@ class RedWebFF:
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
         args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64,
-                           math=K.encoder_math(self.enc_math, B * h * w))
+                           math=K.encoder_math(self.enc_math, B * h * w,
+                                               getattr(self, "x3_min_population", None)))
         K.conv2d_fwd(args, self.stem.w_nat, self.stem.b, A["conv1_pre"])
         self.stem_bn.stats_(A["conv1_pre"], B * h * w, training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
