@@ -415,11 +415,21 @@ class EffNetFF:
                    hw=a.shape[1] * a.shape[2])
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dpred):
-        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params)."""
+    def param_offset(self, name):
+        """Offset of a trainable tensor in the flat params / grads buffers."""
+        return next(off for n, _, off in self.params.specs if n == name)
+
+    def backward(self, dpred, grad_ready=None):
+        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params).
+        grad_ready(offset), if given, is called (in stream order) as soon as every gradient at
+        flat offsets >= offset is final AND the parameters there are no longer read by the rest
+        of the backward (after each decoder layer's dgrad), so a data-parallel caller can reduce
+        and apply those while the rest of the backward runs (the decoder holds 99.6 % of
+        the gradient bytes, the encoder's BN parameters the rest)."""
         A, G, B = self.act, self.gact, self.B
         a = K.conv_args
         h, w = self.H, self.W
+        ready = grad_ready or (lambda off: None)
         # final conv (bias, no BN)
         pt, _ = same_pad(h, 3, 1)
         pl, _ = same_pad(w, 3, 1)
@@ -428,6 +438,9 @@ class EffNetFF:
         K.conv2d_wgrad(args, dpred, self.final.dw)
         K.channel_sum(dpred, B * h * w, 1, self.final.db)
         K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
+        # after the layer's dgrad: its filter copies are no longer read this step (a caller
+        # may update and refresh them from here on)
+        ready(self.param_offset("dec_conv5/kernel"))
         for i in range(len(self.dec) - 1, -1, -1):
             conv, bn, skip = self.dec[i]
             h, w = h // 2, w // 2
@@ -448,6 +461,7 @@ class EffNetFF:
             K.conv2d_wgrad(args, gpre, conv.dw)
             K.channel_sum(gpre, rows, conv.cout, conv.db)
             K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
+            ready(self.param_offset(f"dec_conv{i}/kernel"))
         # encoder
         h, w = A["top_pre"].shape[1:3]
         rows = B * h * w
@@ -463,6 +477,7 @@ class EffNetFF:
             self._block_bwd(blk, x_in, gx_in)
         rows = B * A["stem_pre"].shape[1] * A["stem_pre"].shape[2]
         self.stem_bn.bwd(A["stem_pre"], G["stem_activation"], rows, "swish", None)
+        ready(0)
 
     def _block_bwd(self, blk, x_in, gx_in):
         A, G, B, n = self.act, self.gact, self.B, blk["name"]

@@ -350,8 +350,15 @@ class RedWebFF:
         if gx is not None:
             K.conv2d_dgrad(args, gy, conv.w_dg, gx, None, acc1=gx_acc)
 
-    def backward(self, dpred):
+    def param_offset(self, name):
+        """Offset of a trainable tensor in the flat params / grads buffers."""
+        return next(off for n, _, off in self.params.specs if n == name)
+
+    def backward(self, dpred, grad_ready=None):
+        """grad_ready(offset): as EffNetFF.backward — called once the decoder's gradients (the
+        tail of the flat buffer, from its first trainable conv on) are final, and at the end."""
         A, G, B = self.act, self.gact, self.B
+        ready = grad_ready or (lambda off: None)
         H, W = self.H, self.W
         h, w = H // 2, W // 2
         # AdaptiveOutputLayer
@@ -367,6 +374,8 @@ class RedWebFF:
             up = A["conv5_up"] if i == 0 else A[self.ffls[i - 1]["name"] + "/out"]
             gup = G["conv5_up"] if i == 0 else G[self.ffls[i - 1]["name"] + "/out"]
             self._ffl_bwd(d, A[d["tap"]], G[d["tap"]], up, gup)
+        ready(min(off for n, _, off in self.params.specs
+                  if any(c.trainable and n == c.wk for c in self.convs)))
         K.upsample2x_bwd(G["conv5_up"], G["conv5_block3_out"])
         # encoder (taps already hold their decoder gradient: accumulate onto them)
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -379,6 +388,7 @@ class RedWebFF:
         hp, wp = A["pool1_pool"].shape[1:3]
         K.maxpool2d_bwd(G["pool1_pool"], self.pool_argmax, 3, 2, 1, 1, G["conv1_relu"])
         self.stem_bn.bwd(A["conv1_pre"], G["conv1_relu"], B * h * w, "relu", None)
+        ready(0)
 
     def _block_bwd(self, blk, x, gx, gx_is_tap):
         A, G, B, n = self.act, self.gact, self.B, blk["name"]

@@ -8,9 +8,16 @@ all-reduce the reference never had: one process per GPU, torch.di
 "nccl" backend (= RCCL over xGMI), per-rank batch B, BN statistics per replica (MirroredStrategy
 semantics), one fp32 all-reduce of the flat gradient buffer, 1/world folded into Adam.
 
-Graph structure: the whole step is stream-ordered HIP work with no host synchronisation, captured
-once into hipGraphs (N = 1: one graph; N > 1: [sampler + fwd + bwd] -> all-reduce -> [Adam +
-filter refresh + step++]). Per-step scalars (learning rate, step counter) live in device memory.
+Stepping: the whole step is stream-ordered HIP work with no host synchronisation. N = 1: one
+hipGraph per step (captured after a first eager step). N > 1: eager launches (the host issues a
+step in less time than the GPU runs it: graph and eager steps measure the same throughput), with
+the gradient exchange overlapped with the backward: the backward reports, layer by layer, which
+tail of the flat gradient buffer is final (engine.backward(grad_ready=...)); each ~8 MB bucket
+is all-reduced asynchronously as it completes (RCCL on its own stream) and a side stream runs
+that bucket's Adam-AMSGrad + filter refresh as soon as it lands, while the compute stream carries
+on with the rest of the backward (the decoder holds 99.6 % of the gradient bytes and finishes
+before the encoder backward starts). Per-step scalars (learning rate, step counter) live in
+device memory.
 """
 import numpy as np
 import torch
@@ -70,6 +77,7 @@ class ReplicaTrainer:
         self.m, self.v, self.vhat = self.engine.adam_state()
         self.graphs = None
         self.stream = torch.cuda.Stream(device=dev)
+        self.side = torch.cuda.Stream(device=dev)  # per-bucket optimizer updates (N > 1)
 
     # ------------------------------------------------------------------ data
     def set_batch(self, images, gt, mask):
@@ -140,20 +148,65 @@ class ReplicaTrainer:
         eng.refresh_trainable()
         K.step_increment(self.step_dev)
 
-    def _allreduce(self):
-        if self.world > 1:
-            if not hasattr(self, "_reducer"):
-                from .dp import GradientAllReducer
-                self._reducer = GradientAllReducer(self.engine.grads.buf, self.pg)
-            self._reducer()
+    # ------------------------------------------------------------------ data parallel
+    BUCKET_BYTES = 8 << 20
+
+    def _dp_refresh_convs(self, lo, hi):
+        """Trainable convs whose kernel lies in flat range [lo, hi)."""
+        eng = self.engine
+        return [c for c in eng.convs if c.trainable and lo <= eng.param_offset(c.wk) < hi]
+
+    def _dp_bucket(self, lo, hi):
+        """All-reduce grads[lo:hi) (async, ordered after the compute stream's work so far), then
+        on the side stream: wait for it, Adam-AMSGrad of that range (grad_scale 1/world), refresh
+        of the native filter copies of the convs in it."""
+        import torch.distributed as dist
+        eng = self.engine
+        g = eng.grads.buf[lo:hi]
+        work = dist.all_reduce(g, group=self.pg, async_op=True)
+        b1, b2, eps = self.betas
+        with torch.cuda.stream(self.side):
+            work.wait()
+            K.adam_amsgrad_dev(eng.params.buf[lo:hi], g, self.m[lo:hi], self.v[lo:hi],
+                               self.vhat[lo:hi], self.lr_dev, self.step_dev, b1, b2, eps,
+                               grad_scale=1.0 / self.world)
+            for c in self._dp_refresh_convs(lo, hi):
+                c.refresh()
+        self._dp_works.append(work)
+
+    def _dp_grad_ready(self, off):
+        """engine.backward hook: grads[off:] are final. Launch a bucket once >= BUCKET_BYTES are
+        pending, and always for the last (offset 0) call."""
+        pending = (self._dp_hi - off) * 4
+        if off < self._dp_hi and (pending >= self.BUCKET_BYTES or off == 0):
+            self._dp_bucket(off, self._dp_hi)
+            self._dp_hi = off
+
+    def _step_dp(self):
+        """One data-parallel step (N > 1), eager, on self.stream (+ RCCL and the side stream)."""
+        eng = self.engine
+        self._sample()
+        eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
+        K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
+                          dpred=self.dpred, nll=self.nll, loss=self.loss, zero_dpred=True)
+        self.side.wait_stream(self.stream)
+        self._dp_hi, self._dp_works = eng.grads.buf.numel(), []
+        eng.backward(self.dpred, grad_ready=self._dp_grad_ready)
+        self._dp_grad_ready(0)
+        # the step counter (Adam's bias correction, the next step's Philox keys) advances once
+        # every bucket's update has run; the next step's forward reads the updated filters
+        self.stream.wait_stream(self.side)
+        K.step_increment(self.step_dev)
 
     # ------------------------------------------------------------------ driving
     def step_eager(self, lr):
         with torch.cuda.stream(self.stream):
             K.set_scalar(self.lr_dev, lr)
+            if self.world > 1:
+                self._step_dp()
+                return
             self._sample()
             self._fwd_bwd()
-            self._allreduce()
             self._update()
 
     def capture(self):
@@ -166,15 +219,12 @@ class ReplicaTrainer:
             warnings.warn("hipGraph capture skipped: set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before "
                           "the first GPU call (see pldepth_amd/__init__.py); stepping eagerly")
             return
+        if self.world > 1:
+            return  # data-parallel steps stay eager (see the module docstring)
         torch.cuda.synchronize()
         with torch.cuda.stream(self.stream):
-            if self.world == 1:
-                g = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd(), self._update()))
-                self.graphs = [g]
-            else:
-                ga = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd()))
-                gb = K.Graph().capture(self._update)
-                self.graphs = [ga, gb]
+            g = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd(), self._update()))
+            self.graphs = [g]
         torch.cuda.synchronize()
 
     def step(self, lr):
@@ -183,9 +233,6 @@ class ReplicaTrainer:
         with torch.cuda.stream(self.stream):
             K.set_scalar(self.lr_dev, lr)
             self.graphs[0].launch()
-            if self.world > 1:
-                self._allreduce()
-                self.graphs[1].launch()
 
     def loss_value(self):
         torch.cuda.current_stream().wait_stream(self.stream)
