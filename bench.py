@@ -91,13 +91,36 @@ def profile_conv(trainer, lr):
             return r
         return w
 
+    # the fused BN+ReLU -> upsample -> final 3x3 conv (csrc/upconv.hip): direct VALU kernels
+    up_orig = {n: getattr(K, n) for n in ("upconv_fwd", "upconv_wgrad", "upconv_dgrad")}
+
+    def up_wrap(name, mode):
+        fn = up_orig[name]
+
+        def w(*args, **kw):
+            x = args[0] if mode != 1 else args[2]  # dgrad: (dy, wt, dact) -> dact is [n,h,w,c]
+            n_, h_, w_, c_ = x.shape
+            fl = 2.0 * n_ * (2 * h_) * (2 * w_) * 9 * c_
+            by = 4.0 * (n_ * h_ * w_ * c_ + n_ * 4 * h_ * w_ + 9 * c_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            r = fn(*args, **kw)
+            e1.record(st)
+            recs.append((name + "_kernel", 2, mode, fl, by, e0, e1))
+            return r
+        return w
+
     for n in orig:
         setattr(K, n, wrap(n))
+    for n, m in (("upconv_fwd", 0), ("upconv_dgrad", 1), ("upconv_wgrad", 2)):
+        setattr(K, n, up_wrap(n, m))
     try:
         trainer.step_eager(lr)
         st.synchronize()
     finally:
         for n, f in orig.items():
+            setattr(K, n, f)
+        for n, f in up_orig.items():
             setattr(K, n, f)
     return [(n, k, m, f, b, e0.elapsed_time(e1) / 1e3) for n, k, m, f, b, e0, e1 in recs]
 

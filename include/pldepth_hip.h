@@ -250,6 +250,25 @@ int pld_upsample2x_fwd_bn(const float* x, int n, int h, int w, int c, const floa
                           float* y, void* stream);
 int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx, int accumulate,
                        void* stream);
+
+/* The ff_effnet decoder's last stage fused (pl_hourglass.py:92-96: BatchNormalization -> ReLU ->
+ * UpSampling2D(bilinear) -> Conv2D(1, 3x3, 'same') + bias), without materialising the 2x map:
+ * x [n][h][w][c] is the pre-BN map (c % 4 == 0, c <= 32), BN with the batch statistics
+ * (mean, invstd) and gamma/beta; wt [3][3][c] (HWIO, cout 1); y / dy [n][2h][2w].
+ *   fwd  : y = conv(up(relu(bn(x)))) + bias          (the 2x map bit-identical to
+ *          pld_upsample2x_fwd_bn's)
+ *   wgrad: dw [3][3][c] = d loss / d wt (caller workspace: pld_upconv_wgrad_workspace_size)
+ *   dgrad: dact [n][h][w][c] = up^T(conv^T(dy)): the gradient w.r.t. relu(bn(x)), i.e.
+ *          pld_conv2d_dgrad into the 2x map followed by pld_upsample2x_bwd */
+size_t pld_upconv_wgrad_workspace_size(int c);
+int pld_upconv_fwd(const float* x, int n, int h, int w, int c, const float* mean,
+                   const float* invstd, const float* gamma, const float* beta, const float* wt,
+                   const float* bias, float* y, void* stream);
+int pld_upconv_wgrad(const float* x, int n, int h, int w, int c, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, const float* dy,
+                     float* dw, void* ws, size_t ws_bytes, void* stream);
+int pld_upconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wt, float* dact,
+                     void* stream);
 /* y = a * sample_scale[img] + b  (EfficientNet drop-connect Dropout(noise_shape=(N,1,1,1)) +
  * residual add); sample_scale may be NULL (=1). rows_per_img*c elements per image. */
 int pld_residual_add(const float* a, const float* sample_scale, const float* b, int n,

@@ -462,6 +462,9 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
           bl[b] = lds_frag(B + S::B_PLANE, r, 2 * s + h);
         }
       }
+      // keep the substep's fragment reads together ahead of its MFMAs (one LDS wait per
+      // substep instead of the scheduler's register-saving read-wait-MFMA interleave)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll

@@ -513,6 +513,30 @@ def upsample2x_bwd(dy, dx, accumulate=False):
     return dx
 
 
+def upconv_fwd(x, bn, wt, bias, y):
+    """y [n,2h,2w,1] = conv3x3(up2x(relu(bn(x)))) + bias; bn = (mean, invstd, gamma, beta)."""
+    n, h, w, c = x.shape
+    mean, invstd, gamma, beta = bn
+    lib().pld_upconv_fwd(ptr(x), n, h, w, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                         ptr(wt), ptr(bias), ptr(y), stream())
+    return y
+
+
+def upconv_wgrad(x, bn, dy, dw):
+    n, h, w, c = x.shape
+    mean, invstd, gamma, beta = bn
+    need = lib().pld_upconv_wgrad_workspace_size(c)
+    ws = workspace(need, "upconv")
+    lib().pld_upconv_wgrad(ptr(x), n, h, w, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                           ptr(dy), ptr(dw), ptr(ws), need, stream())
+
+
+def upconv_dgrad(dy, wt, dact):
+    """dact [n,h,w,c] = up2x^T(conv3x3^T(dy)) for dy [n,2h,2w,1], wt [3,3,c,1] (HWIO)."""
+    n, h, w, c = dact.shape
+    lib().pld_upconv_dgrad(ptr(dy), n, h, w, c, ptr(wt), ptr(dact), stream())
+
+
 def residual_add(a, sample_scale, b, y):
     n = a.shape[0]
     lib().pld_residual_add(ptr(a), ptr(sample_scale), ptr(b), n, a.numel() // n, ptr(y),

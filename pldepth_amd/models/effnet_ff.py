@@ -113,6 +113,9 @@ class EffNetFF:
         self._alloc_activations()
         self.drop_connect = True
         self.seed = seed
+        # training: the last decoder stage's upsample runs inside the final conv's kernels
+        # (csrc/upconv.hip); False = the unfused upsample2x + 3x3 conv path
+        self.fuse_final = True
 
     # ------------------------------------------------------------------ graph structure
     def _build_spec(self):
@@ -329,7 +332,9 @@ class EffNetFF:
             K.conv2d_fwd(args, conv.w_nat, conv.b, A[f"dec{i}_pre"])
             rows = B * h * w
             bn.stats_(A[f"dec{i}_pre"], rows, training)
-            if training:
+            if training and i == len(self.dec) - 1 and self.fuse_final:
+                pass  # BN + ReLU + upsample folded into the final conv (upconv_fwd below)
+            elif training:
                 # BN + ReLU applied as the upsampling reads its taps: dec{i}_act is never
                 # materialised (backward re-derives it from dec{i}_pre)
                 K.upsample2x_fwd(A[f"dec{i}_pre"], A[f"dec{i}_up"],
@@ -339,6 +344,12 @@ class EffNetFF:
                 K.upsample2x_fwd(A[f"dec{i}_act"], A[f"dec{i}_up"])
             h, w = 2 * h, 2 * w
             x, x2 = A[f"dec{i}_up"], (A[skip] if skip else None)
+        if training and self.fuse_final:
+            # dec_conv5(up(relu(bn4(dec4_pre)))): the 448^2 x 32 map is never written
+            _, bn4, _ = self.dec[-1]
+            K.upconv_fwd(A["dec4_pre"], (bn4.mean, bn4.invstd, bn4.gamma, bn4.beta),
+                         self.final.w_nat, self.final.b, A["pred"])
+            return A["pred"]
         pt, _ = same_pad(h, 3, 1)
         pl, _ = same_pad(w, 3, 1)
         K.conv2d_fwd(a(x, None, 3, 3, 1, pt, pl, h, w, 1, math=self.dec_math), self.final.w_nat,
@@ -431,20 +442,30 @@ class EffNetFF:
         h, w = self.H, self.W
         ready = grad_ready or (lambda off: None)
         # final conv (bias, no BN)
-        pt, _ = same_pad(h, 3, 1)
-        pl, _ = same_pad(w, 3, 1)
-        x4 = A["dec4_up"]
-        args = a(x4, None, 3, 3, 1, pt, pl, h, w, 1, math=self.dec_math)
-        K.conv2d_wgrad(args, dpred, self.final.dw)
-        K.channel_sum(dpred, B * h * w, 1, self.final.db)
-        K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
+        last = len(self.dec) - 1
+        if self.fuse_final:
+            # through the fused upsample: dec4's activation gradient straight from dpred
+            _, bn4, _ = self.dec[last]
+            K.upconv_wgrad(A["dec4_pre"], (bn4.mean, bn4.invstd, bn4.gamma, bn4.beta), dpred,
+                           self.final.dw)
+            K.channel_sum(dpred, B * h * w, 1, self.final.db)
+            K.upconv_dgrad(dpred, self.final.w_nat, G[f"dec{last}_act"])
+        else:
+            pt, _ = same_pad(h, 3, 1)
+            pl, _ = same_pad(w, 3, 1)
+            x4 = A["dec4_up"]
+            args = a(x4, None, 3, 3, 1, pt, pl, h, w, 1, math=self.dec_math)
+            K.conv2d_wgrad(args, dpred, self.final.dw)
+            K.channel_sum(dpred, B * h * w, 1, self.final.db)
+            K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
         # after the layer's dgrad: its filter copies are no longer read this step (a caller
         # may update and refresh them from here on)
         ready(self.param_offset("dec_conv5/kernel"))
         for i in range(len(self.dec) - 1, -1, -1):
             conv, bn, skip = self.dec[i]
             h, w = h // 2, w // 2
-            K.upsample2x_bwd(G[f"dec{i}_up"], G[f"dec{i}_act"])
+            if not (i == last and self.fuse_final):
+                K.upsample2x_bwd(G[f"dec{i}_up"], G[f"dec{i}_act"])
             rows = B * h * w
             gpre = self._gpre_buf(A[f"dec{i}_pre"].shape)
             bn.bwd(A[f"dec{i}_pre"], G[f"dec{i}_act"], rows, "relu", gpre)

@@ -785,3 +785,57 @@ def test_thin_1x1_conv(cuda, n, h, w, cin, cout):
     K.conv2d_dgrad(args, dev(dy, cuda), K.filter_to_dgrad(gw), dx, None, acc1=True)
     torch.cuda.synchronize()
     assert rel_err(dx - 0.25, dx_ref) < 1e-5, rel_err(dx - 0.25, dx_ref)
+
+
+# ------------------------------------------------- fused BN+ReLU -> upsample x2 -> 3x3 conv to 1
+@pytest.mark.parametrize("n,h,w,c", [(2, 5, 7, 8), (1, 16, 16, 32), (2, 33, 20, 32),
+                                     (2, 224, 224, 32)])
+def test_upconv_matches_unfused_path(cuda, n, h, w, c):
+    """pld_upconv_{fwd,wgrad,dgrad} (csrc/upconv.hip) against the unfused kernels they replace:
+    pld_upsample2x_fwd_bn + pld_conv2d_fwd / _wgrad / _dgrad + pld_upsample2x_bwd."""
+    g = torch.Generator(device=cuda).manual_seed(n * h + w)
+    x = torch.randn(n, h, w, c, device=cuda, generator=g)
+    mean = torch.randn(c, device=cuda, generator=g) * 0.1
+    invstd = torch.rand(c, device=cuda, generator=g) + 0.5
+    gamma = torch.rand(c, device=cuda, generator=g) + 0.5
+    beta = torch.randn(c, device=cuda, generator=g) * 0.1
+    bn = (mean, invstd, gamma, beta)
+    wt = torch.randn(3, 3, c, 1, device=cuda, generator=g) / (9 * c) ** 0.5
+    bias = torch.randn(1, device=cuda, generator=g)
+    dy = torch.randn(n, 2 * h, 2 * w, 1, device=cuda, generator=g)
+    # unfused reference
+    up = torch.empty(n, 2 * h, 2 * w, c, device=cuda)
+    K.upsample2x_fwd(x, up, bn=bn, act="relu")
+    args = K.conv_args(up, None, 3, 3, 1, 1, 1, 2 * h, 2 * w, 1, math="fp32")
+    wn, wd = K.filter_to_native(wt), K.filter_to_dgrad(wt)
+    y_ref = torch.empty(n, 2 * h, 2 * w, 1, device=cuda)
+    K.conv2d_fwd(args, wn, bias, y_ref)
+    dw_ref = torch.empty_like(wt)
+    K.conv2d_wgrad(args, dy, dw_ref)
+    dup = torch.empty_like(up)
+    K.conv2d_dgrad(args, dy, wd, dup)
+    dact_ref = torch.empty_like(x)
+    K.upsample2x_bwd(dup, dact_ref)
+    # fused
+    y = torch.empty_like(y_ref)
+    K.upconv_fwd(x, bn, wn, bias, y)
+    dw = torch.empty_like(wt)
+    K.upconv_wgrad(x, bn, dy, dw)
+    dact = torch.empty_like(x)
+    K.upconv_dgrad(dy, wt, dact)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-6
+    assert rel_err(dw, dw_ref) < 1e-5
+    assert rel_err(dact, dact_ref) < 1e-5
+    # and against torch-CPU fp64 for the whole composition
+    x64 = x.double().cpu().permute(0, 3, 1, 2)
+    a = torch.relu((x64 - mean.double().cpu().view(1, -1, 1, 1)) *
+                   invstd.double().cpu().view(1, -1, 1, 1) * gamma.double().cpu().view(1, -1, 1, 1)
+                   + beta.double().cpu().view(1, -1, 1, 1)).requires_grad_(True)
+    u = F.interpolate(a, scale_factor=2, mode="bilinear", align_corners=False)
+    w64 = wt.double().cpu().permute(3, 2, 0, 1).requires_grad_(True)
+    o = F.conv2d(u, w64, bias.double().cpu(), padding=1)
+    o.backward(dy.double().cpu().permute(0, 3, 1, 2))
+    assert rel_err(y, o.detach().permute(0, 2, 3, 1)) < 1e-5
+    assert rel_err(dw, w64.grad.permute(2, 3, 1, 0)) < 1e-5
+    assert rel_err(dact, a.grad.permute(0, 2, 3, 1)) < 1e-5
