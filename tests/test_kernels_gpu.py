@@ -833,7 +833,7 @@ def test_upconv_matches_unfused_path(cuda, n, h, w, c):
                    invstd.double().cpu().view(1, -1, 1, 1) * gamma.double().cpu().view(1, -1, 1, 1)
                    + beta.double().cpu().view(1, -1, 1, 1)).requires_grad_(True)
     u = F.interpolate(a, scale_factor=2, mode="bilinear", align_corners=False)
-    w64 = wt.double().cpu().permute(3, 2, 0, 1).requires_grad_(True)
+    w64 = wt.double().cpu().permute(3, 2, 0, 1).contiguous().requires_grad_(True)
     o = F.conv2d(u, w64, bias.double().cpu(), padding=1)
     o.backward(dy.double().cpu().permute(0, 3, 1, 2))
     assert rel_err(y, o.detach().permute(0, 2, 3, 1)) < 1e-5
