@@ -91,17 +91,23 @@ def profile_conv(trainer, lr):
             return r
         return w
 
-    # the fused BN+ReLU -> upsample -> final 3x3 conv (csrc/upconv.hip): direct VALU kernels
-    up_orig = {n: getattr(K, n) for n in ("upconv_fwd", "upconv_wgrad", "upconv_dgrad")}
+    # the fused BN+ReLU -> upsample -> final 3x3 conv (csrc/upconv.hip): direct VALU kernels.
+    # Algorithmic FLOPs are the conv's own (2 per MAC over the 2x map, per fwd / dX / dW pass:
+    # the SURVEY §8d count); bytes: x (or dact) + the 1-channel 2x map + the filter.
+    up_orig = {n: getattr(K, n) for n in ("upconv_fwd", "upconv_wgrad", "upconv_dgrad",
+                                          "upconv_bwd")}
 
     def up_wrap(name, mode):
         fn = up_orig[name]
 
         def w(*args, **kw):
-            x = args[0] if mode != 1 else args[2]  # dgrad: (dy, wt, dact) -> dact is [n,h,w,c]
+            # dgrad: (dy, wt, dact) -> dact is [n,h,w,c]; bwd: (x, bn, wt, dy, dact, ...)
+            x = args[2] if name == "upconv_dgrad" else args[0]
             n_, h_, w_, c_ = x.shape
-            fl = 2.0 * n_ * (2 * h_) * (2 * w_) * 9 * c_
-            by = 4.0 * (n_ * h_ * w_ * c_ + n_ * 4 * h_ * w_ + 9 * c_)
+            passes = 2 if name == "upconv_bwd" else 1  # bwd: dX and dW in one pass
+            fl = passes * 2.0 * n_ * (2 * h_) * (2 * w_) * 9 * c_
+            by = 4.0 * (n_ * h_ * w_ * c_ * (2 if name == "upconv_bwd" else 1)
+                        + n_ * 4 * h_ * w_ + 9 * c_)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             r = fn(*args, **kw)
@@ -112,7 +118,8 @@ def profile_conv(trainer, lr):
 
     for n in orig:
         setattr(K, n, wrap(n))
-    for n, m in (("upconv_fwd", 0), ("upconv_dgrad", 1), ("upconv_wgrad", 2)):
+    for n, m in (("upconv_fwd", 0), ("upconv_dgrad", 1), ("upconv_wgrad", 2),
+                 ("upconv_bwd", 1)):
         setattr(K, n, up_wrap(n, m))
     try:
         trainer.step_eager(lr)

@@ -252,18 +252,30 @@ int pld_upsample2x_bwd(const float* dy, int n, int h, int w, int c, float* dx, i
                        void* stream);
 
 /* The ff_effnet decoder's last stage fused (pl_hourglass.py:92-96: BatchNormalization -> ReLU ->
- * UpSampling2D(bilinear) -> Conv2D(1, 3x3, 'same') + bias), without materialising the 2x map:
+ * UpSampling2D(bilinear) -> Conv2D(1, 3x3, 'same') + bias), without forming the 2x map:
  * x [n][h][w][c] is the pre-BN map (c % 4 == 0, c <= 32), BN with the batch statistics
- * (mean, invstd) and gamma/beta; wt [3][3][c] (HWIO, cout 1); y / dy [n][2h][2w].
- *   fwd  : y = conv(up(relu(bn(x)))) + bias          (the 2x map bit-identical to
- *          pld_upsample2x_fwd_bn's)
- *   wgrad: dw [3][3][c] = d loss / d wt (caller workspace: pld_upconv_wgrad_workspace_size)
- *   dgrad: dact [n][h][w][c] = up^T(conv^T(dy)): the gradient w.r.t. relu(bn(x)), i.e.
- *          pld_conv2d_dgrad into the 2x map followed by pld_upsample2x_bwd */
+ * (mean, invstd) and gamma/beta (16-byte aligned); wt [3][3][c] (HWIO, cout 1); y / dy
+ * [n][2h][2w]. The one-channel conv commutes with the per-channel upsampling: the kernels work
+ * on the 9 tap maps z_t = sum_c w_t[c] relu(bn(x))_c (forward) and G_t = up^T(shift_t^T dy)
+ * (backward) at 1x resolution.
+ *   fwd  : y = conv(up(relu(bn(x)))) + bias    (replaces pld_upsample2x_fwd_bn + pld_conv2d_fwd)
+ *   bwd  : dact [n][h][w][c] = up^T(conv^T(dy)) (the gradient w.r.t. relu(bn(x)); NULL = not
+ *          wanted), dw [3][3][c] = d loss / d wt (NULL = not wanted), and, when dx is given, the
+ *          whole BatchNormalization + ReLU backward of x as pld_bn_bwd(x, dact, ..., act relu)
+ *          computes it (dx =|+= , dgamma/dbeta =|+= by param_accumulate), its channel
+ *          reductions accumulated inside the same pass (dact must then be given: the apply reads
+ *          it). Caller workspace: pld_upconv_bwd_workspace_size(c) when dw or dx is wanted.
+ *   wgrad / dgrad: pld_upconv_bwd with only dw / only dact (wgrad's workspace size is bwd's). */
+size_t pld_upconv_bwd_workspace_size(int c);
 size_t pld_upconv_wgrad_workspace_size(int c);
 int pld_upconv_fwd(const float* x, int n, int h, int w, int c, const float* mean,
                    const float* invstd, const float* gamma, const float* beta, const float* wt,
                    const float* bias, float* y, void* stream);
+int pld_upconv_bwd(const float* x, int n, int h, int w, int c, const float* mean,
+                   const float* invstd, const float* gamma, const float* beta, const float* wt,
+                   const float* dy, float* dact, float* dw, float* dx, int dx_accumulate,
+                   float* dgamma, float* dbeta, int param_accumulate, void* ws, size_t ws_bytes,
+                   void* stream);
 int pld_upconv_wgrad(const float* x, int n, int h, int w, int c, const float* mean,
                      const float* invstd, const float* gamma, const float* beta, const float* dy,
                      float* dw, void* ws, size_t ws_bytes, void* stream);

@@ -75,6 +75,9 @@ _SIGS = {
     "pld_upsample2x_fwd_bn": (I32, [P, I32, I32, I32, I32, P, P, P, P, I32, P, P]),
     "pld_upsample2x_bwd": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "pld_upconv_wgrad_workspace_size": (SZ, [I32]),
+    "pld_upconv_bwd_workspace_size": (SZ, [I32]),
+    "pld_upconv_bwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, I32, P, P, I32, P,
+                             SZ, P]),
     "pld_upconv_fwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P]),
     "pld_upconv_wgrad": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, SZ, P]),
     "pld_upconv_dgrad": (I32, [P, I32, I32, I32, I32, P, P, P]),
@@ -114,7 +117,8 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",
-               "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size"}
+               "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",
+               "pld_upconv_bwd_workspace_size"}
 
 
 def declared_symbols(header=HEADER):

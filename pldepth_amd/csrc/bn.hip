@@ -579,6 +579,13 @@ extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const
   return check_launch("bn_apply_kernel(affine)");
 }
 
+static int bn_bwd_finish(const double* part, int nbx, const float* x, const float* dy,
+                         int64_t rows, int c, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int act, const float* gate,
+                         const float* addn, FastDiv dHW, const float* res, float* dx,
+                         int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st);
+
 static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, const float* mean,
                        const float* invstd, const float* gamma, const float* beta, int act,
                        const float* gate, const float* addn, int hw, const float* res,
@@ -610,9 +617,22 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
   float* k12 = reinterpret_cast<float*>((char*)ws + red_ws_doubles(rows, c) * sizeof(double));
-  bnbwd_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
+  return bn_bwd_finish(p.partial, nbx, x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn,
+                       p.dHW, res, dx, dx_accumulate, dres, dres_accumulate, dgamma, dbeta,
+                       param_accumulate, k12, st);
+}
+
+// finalize (dgamma, dbeta, k1 = mean dz, k2 = mean dz xhat from nbx channel-major partials) +
+// the elementwise dx / dres pass
+static int bn_bwd_finish(const double* part, int nbx, const float* x, const float* dy,
+                         int64_t rows, int c, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int act, const float* gate,
+                         const float* addn, FastDiv dHW, const float* res, float* dx,
+                         int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st) {
+  bnbwd_finalize_kernel<<<c, 256, 0, st>>>(part, nbx, c, rows, dgamma, dbeta,
                                                        param_accumulate, k12);
-  rc = check_launch("bnbwd_finalize_kernel");
+  int rc = check_launch("bnbwd_finalize_kernel");
   if (rc || !(dx || dres)) return rc;
   BwdApplyParams q{};
   q.x = x;
@@ -626,7 +646,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
   q.act = act;
   q.gate = gate;
   q.addn = addn;
-  q.dHW = p.dHW;
+  q.dHW = dHW;
   q.k12 = k12;
   q.dx = dx;
   q.acc = dx_accumulate;
@@ -640,6 +660,20 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
     bn_bwd_apply_kernel<1><<<ew_grid_c(rows * c, c), 256, 0, st>>>(q);
   }
   return check_launch("bn_bwd_apply_kernel");
+}
+
+// internal (upconv.hip): the BN backward from partials a producer kernel accumulated
+extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
+                                  int64_t rows, int c, const float* mean, const float* invstd,
+                                  const float* gamma, const float* beta, int act, float* dx,
+                                  int dx_accumulate, float* dgamma, float* dbeta,
+                                  int param_accumulate, float* k12, hipStream_t st) {
+  PLD_CHECK_ARG(part && x && dy && mean && invstd && gamma && beta && k12 && rows > 0 && c > 0,
+                "pld__bn_bwd_finish: bad args");
+  PLD_CHECK_ARG(rows * c < (1L << 31), "pld__bn_bwd_finish: tensor too large");
+  return bn_bwd_finish(part, nparts, x, dy, rows, c, mean, invstd, gamma, beta, act, nullptr,
+                       nullptr, FastDiv(1), nullptr, dx, dx_accumulate, nullptr, 0, dgamma, dbeta,
+                       param_accumulate, k12, st);
 }
 
 extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,

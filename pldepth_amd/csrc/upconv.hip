@@ -1,17 +1,21 @@
 // The ff_effnet decoder's last stage fused: BN + ReLU -> UpSampling2D(bilinear) x2 ->
-// Conv2D(1, 3x3, 'same') + bias (pldepth/models/pl_hourglass.py:92-96), forward, filter gradient
-// and the input gradient taken back through the upsampling, without materialising the 2x map.
+// Conv2D(1, 3x3, 'same') + bias (pldepth/models/pl_hourglass.py:92-96), forward and backward,
+// without materialising the 2x map — and without forming it at all.
 //
-// Unfused, the 448x448x32 upsampled map is written by the upsample (822 MB at batch 32), read by
-// the conv forward and by its filter gradient, and its gradient is written by the conv dgrad and
-// read back by the upsample's adjoint: ~4 passes over 822 MB. Here every kernel reads the
-// 224x224 pre-BN map (or the 1-channel dpred) and builds the part of the 2x map it needs in LDS:
-//   fwd   : y[p] = b + sum_{t,c} w[t][c] * up[p + t - 1][c],  up = bilinear2x(relu(bn(x)))
-//   wgrad : dw[t][c] = sum_p up[p + t - 1][c] * dy[p]  (persistent partials + ordered reduce)
-//   dgrad : dact = bilinear2x^T(dup),  dup[q][c] = sum_t w[t][c] * dy[q - t + 1]
-// The 2x map is formed with the same taps and lerp arithmetic as upsample2x_fwd_cell_kernel
-// (resample.hip), the BN prologue as its UpPro, so `up` is bit-identical to the unfused path's.
-// Algorithmic bytes: fwd/wgrad read x (224^2 x c) once (+ dy), dgrad reads dy and writes dact.
+// The conv has ONE output channel and the upsampling is linear and acts on every channel alike,
+// so the channel contraction commutes with it. With a = relu(bn(x)) on the h x w map, w_t the
+// tap-t filter (t = (ty, tx)), Up the bilinear x2 (TF2 half-pixel, edge-clamped) and S_t the shift
+// by t - 1 (zero outside the 2x map: the conv's 'same' padding):
+//   fwd  : y = b + sum_t S_t Up(z_t),          z_t[q] = sum_c w_t[c] a_c[q]      (9 maps, 1x)
+//   bwd  : G_t = Up^T S_t^T dy                  (9 maps, 1x: a 4x4 adjoint stencil of dy)
+//          dw_t[c] = sum_q a_c[q] G_t[q]        dact_c[q] = sum_t w_t[c] G_t[q]
+// Per 1x pixel that is 9 c MACs each way instead of 9 c MACs per 2x pixel (4x the work) plus the
+// upsampling of c channels; the 2x map (822 MB at 448^2, batch 32) is never touched. The backward
+// kernel also accumulates the training-mode BN backward reductions of the dec4 BN (sum dz,
+// sum dz xhat with dz = dact relu'(bn(x)), chan_reduce's RED_BNBWD arithmetic) from the x and dact
+// it holds, so that BN's backward needs only its finalize + apply (bn.hip).
+// Algorithmic bytes: fwd reads x (+ a 1-pixel halo) and writes y; bwd reads x and dy and writes
+// dact.
 #include <algorithm>
 
 #include "common.h"
@@ -20,14 +24,12 @@ namespace pld {
 namespace upc {
 
 constexpr int NT = 256;
-constexpr int ST = 16;           // 2x-map output tile edge (fwd / wgrad)
-constexpr int UT = ST + 2;       // 2x-map halo edge (3x3)
-constexpr int SR = ST / 2 + 2;   // source rows / cols feeding a UT x UT 2x-map window
-constexpr int CMAX = 32;         // channels (the decoder's dec_conv4 output)
-constexpr int CS = CMAX + 4;     // padded LDS channel stride
-constexpr int DT = 8;            // dgrad: source (1x map) tile edge
-constexpr int DU = 2 * DT + 2;   // its 2x-map window edge
-constexpr int DY = DU + 2;       // the dy window edge feeding that
+constexpr int T = 14;            // 1x-map tile edge
+constexpr int TE = T + 2;        // with the 1-pixel halo: 16 x 16 = NT pixels, one per thread
+constexpr int DW = 2 * T + 4;    // dy window edge feeding a tile's adjoint stencils
+constexpr int CM = 32;           // channels (the decoder's dec_conv4 output)
+constexpr int NQ = CM / 4;
+constexpr int BWD_BLOCKS = 1024; // persistent backward grid (partial slabs: BWD_BLOCKS rows)
 
 struct Params {
   const float* x;       // [n][h][w][c] pre-BN (dec4_pre)
@@ -38,10 +40,12 @@ struct Params {
   const float* wt;      // [3][3][c] (HWIO, cout 1)
   const float* bias;    // [1] or NULL
   const float* dy;      // [n][2h][2w]
-  float* y;             // fwd: [n][2h][2w]; dgrad: dact [n][h][w][c]
-  float* part;          // wgrad partials [gridDim.x][9 c]
+  float* y;             // fwd: [n][2h][2w]
+  float* dact;          // bwd: [n][h][w][c] or NULL
+  float* dwpart;        // bwd: [9 c][gridDim.x] filter-gradient partials, or NULL
+  double* bnpart;       // bwd: [c][gridDim.x][2] BN-backward partials, or NULL
   int n, h, w, c;
-  int tiles_x, tiles_y;  // fwd / wgrad tiles of the 2x map
+  int tiles_x, tiles_y;
 };
 
 __device__ __forceinline__ void lerp_coords(int o, int in_size, int& lo, int& hi, float& l) {
@@ -52,217 +56,304 @@ __device__ __forceinline__ void lerp_coords(int o, int in_size, int& lo, int& hi
   l = in - f;
 }
 
-// source window of a fwd / wgrad tile: rows sy0 .. sy0 + SR - 1 (clamped into the image: the
-// clamped duplicates are what the bilinear taps clamp to), prologued, in registers then LDS
-struct SrcRegs {
-  static constexpr int NQ = CMAX / 4, TOTAL = SR * SR * NQ, IT = (TOTAL + NT - 1) / NT;
-  float4 v[IT];
-  float dy;
-};
+// weight with which 1x row i enters the 2x row u's bilinear tap pair (both taps at a clamp)
+__device__ __forceinline__ float adj_weight(int u, int n1, int i) {
+  int lo, hi;
+  float l;
+  lerp_coords(u, n1, lo, hi, l);
+  return (lo == i ? 1.f - l : 0.f) + (hi == i ? l : 0.f);
+}
 
-__device__ __forceinline__ void tile_origin(const Params& p, int tile, int& img, int& Y0,
-                                            int& X0) {
+__device__ __forceinline__ void tile_origin(const Params& p, int tile, int& img, int& i0,
+                                            int& j0) {
   img = tile / (p.tiles_x * p.tiles_y);
   const int r = tile - img * p.tiles_x * p.tiles_y;
-  Y0 = (r / p.tiles_x) * ST;
-  X0 = (r % p.tiles_x) * ST;
+  i0 = (r / p.tiles_x) * T;
+  j0 = (r % p.tiles_x) * T;
 }
 
-__device__ __forceinline__ void src_load(const Params& p, SrcRegs& s, int tile, bool with_dy) {
-  int img, Y0, X0;
-  tile_origin(p, tile, img, Y0, X0);
-  const int sy0 = Y0 / 2 - 1, sx0 = X0 / 2 - 1;
-  const long img_elems = (long)p.h * p.w * p.c;
-  const float* base = p.x + img * img_elems;
+// BN (batch statistics) + ReLU, upsample2x_fwd_bn's UpPro arithmetic
+__device__ __forceinline__ float bnrelu(float v, float mu, float is, float ga, float be) {
+  return act_fwd(ACT_RELU, ((v - mu) * is) * ga + be);
+}
+
+// per-block constants in LDS: BN parameters and filter taps by channel quad (zero past c)
+struct Consts {
+  float4 mu[NQ], is[NQ], ga[NQ], be[NQ];
+  float4 wq[9][NQ];
+};
+
+__device__ __forceinline__ void load_consts(const Params& p, Consts& k, bool with_bn) {
+  const int tid = threadIdx.x, nq = p.c / 4;
+  if (tid < 9 * NQ) {
+    const int t = tid / NQ, q = tid % NQ;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < nq && p.wt) {  // wt NULL: no dact wanted (filter gradient only)
+      const float* s = p.wt + t * p.c + 4 * q;
+      v = make_float4(s[0], s[1], s[2], s[3]);
+    }
+    k.wq[t][q] = v;
+  } else if (with_bn && tid >= 128 && tid < 128 + 4 * NQ) {
+    const int e = tid - 128, which = e / NQ, q = e % NQ;
+    const float* src = which == 0 ? p.mean : which == 1 ? p.invstd : which == 2 ? p.gamma : p.beta;
+    const float4 v = q < nq ? *reinterpret_cast<const float4*>(src + 4 * q)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    (which == 0 ? k.mu : which == 1 ? k.is : which == 2 ? k.ga : k.be)[q] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------- forward
+// One workgroup per 14 x 14 tile of the 1x map: thread = one pixel of the 16 x 16 halo window,
+// z_t of its pixel into LDS; then the 28 x 28 outputs of the tile, each from the 9 tap maps'
+// bilinear taps (lerp_coords: the upsampling's exact taps and weights).
+__global__ __launch_bounds__(NT) void upconv_fwd_kernel(Params p) {
+  __shared__ float zs[9][TE * TE];
+  __shared__ Consts k;
+  const int tid = threadIdx.x;
+  const int nq = p.c / 4;
+  int img, i0, j0;
+  tile_origin(p, blockIdx.x, img, i0, j0);
+  const int i = i0 - 1 + tid / TE, j = j0 - 1 + tid % TE;
+  const bool in = i >= 0 && i < p.h && j >= 0 && j < p.w;
+  float4 xv[NQ];
+  if (in) {
+    const float4* src =
+        reinterpret_cast<const float4*>(p.x + (((long)img * p.h + i) * p.w + j) * p.c);
 #pragma unroll
-  for (int i = 0; i < SrcRegs::IT; ++i) {
-    const int e = threadIdx.x + NT * i;
-    const int q = e % SrcRegs::NQ, pix = e / SrcRegs::NQ;
-    const int ry = min(max(sy0 + pix / SR, 0), p.h - 1);
-    const int rx = min(max(sx0 + pix % SR, 0), p.w - 1);
-    const bool ok = e < SrcRegs::TOTAL && 4 * q < p.c;
-    s.v[i] = ok ? *reinterpret_cast<const float4*>(base + ((long)ry * p.w + rx) * p.c + 4 * q)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < NQ; ++q) xv[q] = q < nq ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (with_dy) {
-    const int H2 = 2 * p.h, W2 = 2 * p.w;
-    const int oy = Y0 + threadIdx.x / ST, ox = X0 + threadIdx.x % ST;
-    s.dy = (oy < H2 && ox < W2) ? p.dy[((long)img * H2 + oy) * W2 + ox] : 0.f;
-  }
-}
-
-// prologue (BN with batch statistics, then ReLU: UpPro act 1) and the LDS store of the window
-__device__ __forceinline__ void src_store(const Params& p, const SrcRegs& s, float* src) {
+  load_consts(p, k, true);
+  __syncthreads();
+  float z[9];
 #pragma unroll
-  for (int i = 0; i < SrcRegs::IT; ++i) {
-    const int e = threadIdx.x + NT * i;
-    if (e >= SrcRegs::TOTAL) continue;
-    const int q = e % SrcRegs::NQ, pix = e / SrcRegs::NQ;
-    if (4 * q >= p.c) continue;
-    const float4 mu = *reinterpret_cast<const float4*>(p.mean + 4 * q);
-    const float4 is = *reinterpret_cast<const float4*>(p.invstd + 4 * q);
-    const float4 ga = *reinterpret_cast<const float4*>(p.gamma + 4 * q);
-    const float4 be = *reinterpret_cast<const float4*>(p.beta + 4 * q);
-    float4 v = s.v[i];
-    v.x = act_fwd(1, ((v.x - mu.x) * is.x) * ga.x + be.x);
-    v.y = act_fwd(1, ((v.y - mu.y) * is.y) * ga.y + be.y);
-    v.z = act_fwd(1, ((v.z - mu.z) * is.z) * ga.z + be.z);
-    v.w = act_fwd(1, ((v.w - mu.w) * is.w) * ga.w + be.w);
-    *reinterpret_cast<float4*>(src + pix * CS + 4 * q) = v;
-  }
-}
-
-// the UT x UT window of the 2x map at (Y0 - 1, X0 - 1) from the source window in LDS: zeros
-// outside the 2x map (the conv's 'same' padding), else upsample2x_fwd_cell_kernel's taps and
-// top / bottom lerp arithmetic
-__device__ __forceinline__ void build_up(const Params& p, int Y0, int X0, const float* src,
-                                         float* up) {
-  const int H2 = 2 * p.h, W2 = 2 * p.w, nq = p.c / 4;
-  const int sy0 = Y0 / 2 - 1, sx0 = X0 / 2 - 1;
-  for (int e = threadIdx.x; e < UT * UT * nq; e += NT) {
-    const int q = e % nq, pix = e / nq;
-    const int uy = Y0 - 1 + pix / UT, ux = X0 - 1 + pix % UT;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (uy >= 0 && uy < H2 && ux >= 0 && ux < W2) {
-      int y0, y1, x0, x1;
-      float yl, xl;
-      lerp_coords(uy, p.h, y0, y1, yl);
-      lerp_coords(ux, p.w, x0, x1, xl);
-      const float* r0 = src + (y0 - sy0) * SR * CS + 4 * q;
-      const float* r1 = src + (y1 - sy0) * SR * CS + 4 * q;
-      const float4 tl = *reinterpret_cast<const float4*>(r0 + (x0 - sx0) * CS);
-      const float4 tr = *reinterpret_cast<const float4*>(r0 + (x1 - sx0) * CS);
-      const float4 bl = *reinterpret_cast<const float4*>(r1 + (x0 - sx0) * CS);
-      const float4 br = *reinterpret_cast<const float4*>(r1 + (x1 - sx0) * CS);
-      {
-        const float top = tl.x + (tr.x - tl.x) * xl, bot = bl.x + (br.x - bl.x) * xl;
-        o.x = top + (bot - top) * yl;
-      }
-      {
-        const float top = tl.y + (tr.y - tl.y) * xl, bot = bl.y + (br.y - bl.y) * xl;
-        o.y = top + (bot - top) * yl;
-      }
-      {
-        const float top = tl.z + (tr.z - tl.z) * xl, bot = bl.z + (br.z - bl.z) * xl;
-        o.z = top + (bot - top) * yl;
-      }
-      {
-        const float top = tl.w + (tr.w - tl.w) * xl, bot = bl.w + (br.w - bl.w) * xl;
-        o.w = top + (bot - top) * yl;
+  for (int t = 0; t < 9; ++t) z[t] = 0.f;
+  if (in) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q >= nq) break;
+      const float4 mu = k.mu[q], is = k.is[q], ga = k.ga[q], be = k.be[q];
+      float4 a;
+      a.x = bnrelu(xv[q].x, mu.x, is.x, ga.x, be.x);
+      a.y = bnrelu(xv[q].y, mu.y, is.y, ga.y, be.y);
+      a.z = bnrelu(xv[q].z, mu.z, is.z, ga.z, be.z);
+      a.w = bnrelu(xv[q].w, mu.w, is.w, ga.w, be.w);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4 f = k.wq[t][q];
+        z[t] += a.x * f.x + a.y * f.y + a.z * f.z + a.w * f.w;
       }
     }
-    *reinterpret_cast<float4*>(up + pix * CS + 4 * q) = o;
   }
-}
-
-// persistent workgroups over the 2x-map tiles; the next tile's source window is in flight while
-// the current one is computed
-__global__ __launch_bounds__(NT) void upconv_fwd_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) float src[SR * SR * CS];
-  __shared__ __attribute__((aligned(16))) float up[UT * UT * CS];
-  __shared__ __attribute__((aligned(16))) float wl[9 * CMAX];
-  const int tx = threadIdx.x % ST, ty = threadIdx.x / ST;
-  const int ntiles = p.tiles_x * p.tiles_y * p.n;
-  for (int e = threadIdx.x; e < 9 * p.c; e += NT) wl[(e / p.c) * CMAX + e % p.c] = p.wt[e];
-  SrcRegs sr;
-  src_load(p, sr, min((int)blockIdx.x, ntiles - 1), false);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) zs[t][tid] = z[t];
+  __syncthreads();
+  const int H2 = 2 * p.h, W2 = 2 * p.w;
   const float b = p.bias ? p.bias[0] : 0.f;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int img, Y0, X0;
-    tile_origin(p, tile, img, Y0, X0);
-    __syncthreads();
-    src_store(p, sr, src);
-    __syncthreads();
-    src_load(p, sr, min(tile + (int)gridDim.x, ntiles - 1), false);
-    build_up(p, Y0, X0, src, up);
-    __syncthreads();
-    // skinny_fwd_kernel's accumulation: taps, then channel quads
+  for (int o = tid; o < 4 * T * T; o += NT) {
+    const int Y = 2 * i0 + o / (2 * T), X = 2 * j0 + o % (2 * T);
+    if (Y >= H2 || X >= W2) continue;
     float acc = 0.f;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float* hp = up + ((ty + t / 3) * UT + tx + t % 3) * CS;
-      const float* wp = wl + t * CMAX;
-      for (int q = 0; q < p.c; q += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(hp + q);
-        const float4 f = *reinterpret_cast<const float4*>(wp + q);
-        acc += v.x * f.x + v.y * f.y + v.z * f.z + v.w * f.w;
+    for (int ty = 0; ty < 3; ++ty) {
+      const int u = Y + ty - 1;
+      if (u < 0 || u >= H2) continue;
+      int y0, y1;
+      float yl;
+      lerp_coords(u, p.h, y0, y1, yl);
+      const int r0 = (y0 - i0 + 1) * TE, r1 = (y1 - i0 + 1) * TE;
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) {
+        const int v = X + tx - 1;
+        if (v < 0 || v >= W2) continue;
+        int x0, x1;
+        float xl;
+        lerp_coords(v, p.w, x0, x1, xl);
+        const int c0 = x0 - j0 + 1, c1 = x1 - j0 + 1;
+        const float* zt = zs[ty * 3 + tx];
+        const float tl = zt[r0 + c0], tr = zt[r0 + c1], bl = zt[r1 + c0], br = zt[r1 + c1];
+        const float top = tl + (tr - tl) * xl, bot = bl + (br - bl) * xl;
+        acc += top + (bot - top) * yl;
       }
     }
-    const int oy = Y0 + ty, ox = X0 + tx;
-    if (oy < 2 * p.h && ox < 2 * p.w) p.y[((long)img * 2 * p.h + oy) * 2 * p.w + ox] = acc + b;
+    p.y[((long)img * H2 + Y) * W2 + X] = acc + b;
   }
 }
 
-// 256 threads = 8 channel quads x 32 pixel groups of 8 pixels (skinny_wgrad_kernel's layout)
-__global__ __launch_bounds__(NT) void upconv_wgrad_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) float src[SR * SR * CS];
-  __shared__ __attribute__((aligned(16))) float up[UT * UT * CS];
-  __shared__ float dyl[ST * ST];
-  __shared__ __attribute__((aligned(16))) float comb[4][9 * CMAX];
+// --------------------------------------------------------------------------------- backward
+// Persistent workgroups over the 14 x 14 tiles. Per tile: the (2T + 4)^2 dy window into LDS;
+// threads 0..195 form G_t (9 values) of one core pixel from it; then thread (pixel group pg,
+// channel quad q) walks the tile's pixels pg, pg + 32, ...: dact quad, and the running dw and
+// BN-backward sums in registers. End: fixed-order reduction over the workgroup, one partial row
+// per workgroup (reduced in order by upconv_dw_reduce_kernel / bn.hip's finalize).
+__global__ __launch_bounds__(NT) void upconv_bwd_kernel(Params p) {
+  __shared__ float dyl[DW * DW];
+  __shared__ float gs[9][T * T];
+  __shared__ Consts k;
+  __shared__ float4 comb[4][9][NQ];
+  __shared__ double bcomb[4][2][CM];
+  const int tid = threadIdx.x, q = tid & 7, pg = tid >> 3;
+  const int nq = p.c / 4;
+  const bool with_x = p.x != nullptr;
+  const int H2 = 2 * p.h, W2 = 2 * p.w;
   const int ntiles = p.tiles_x * p.tiles_y * p.n;
-  const int q = threadIdx.x & 7, pg = threadIdx.x >> 3;
-  float4 acc[9];
+  load_consts(p, k, with_x);
+  __syncthreads();
+  float4 wv[9], mu = make_float4(0.f, 0.f, 0.f, 0.f), is = mu, ga = mu, be = mu;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-  SrcRegs sr;
-  src_load(p, sr, min((int)blockIdx.x, ntiles - 1), true);
+  for (int t = 0; t < 9; ++t) wv[t] = k.wq[t][q];
+  if (with_x) {
+    mu = k.mu[q];
+    is = k.is[q];
+    ga = k.ga[q];
+    be = k.be[q];
+  }
+  float4 dwacc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) dwacc[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int img, Y0, X0;
-    tile_origin(p, tile, img, Y0, X0);
+    int img, i0, j0;
+    tile_origin(p, tile, img, i0, j0);
+    __syncthreads();  // the previous tile's readers of dyl / gs are done
+    // dyl[r][s] = dy[2 i0 - 2 + r][2 j0 - 2 + s] (0 outside the 2x map)
+    const float* dimg = p.dy + (long)img * H2 * W2;
+    for (int e = tid; e < DW * DW; e += NT) {
+      const int yy = 2 * i0 - 2 + e / DW, xx = 2 * j0 - 2 + e % DW;
+      dyl[e] = (yy >= 0 && yy < H2 && xx >= 0 && xx < W2) ? dimg[(long)yy * W2 + xx] : 0.f;
+    }
     __syncthreads();
-    src_store(p, sr, src);
-    dyl[threadIdx.x] = sr.dy;
+    if (tid < T * T) {
+      const int ci = tid / T, cj = tid % T, i = i0 + ci, j = j0 + cj;
+      float g[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t] = 0.f;
+      if (i < p.h && j < p.w) {
+        // G_t[i][j] = sum_{u, v} Up^T weights * dy[u - ty + 1][v - tx + 1] over the 2x rows
+        // u = 2i - 1 .. 2i + 2 and columns v = 2j - 1 .. 2j + 2 inside the 2x map
+        float wxs[4];
+#pragma unroll
+        for (int dv = -1; dv <= 2; ++dv) {
+          const int v = 2 * j + dv;
+          wxs[dv + 1] = (v >= 0 && v < W2) ? adj_weight(v, p.w, j) : 0.f;
+        }
+#pragma unroll
+        for (int du = -1; du <= 2; ++du) {
+          const int u = 2 * i + du;
+          const float wy = (u >= 0 && u < H2) ? adj_weight(u, p.h, i) : 0.f;
+#pragma unroll
+          for (int dv = -1; dv <= 2; ++dv) {
+            const float ww = wy * wxs[dv + 1];
+            // window row of dy[u - ty + 1]: (u - ty + 1) - (2 i0 - 2) = 2 ci + du - ty + 3
+#pragma unroll
+            for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+              for (int tx = 0; tx < 3; ++tx)
+                g[ty * 3 + tx] +=
+                    ww * dyl[(2 * ci + du - ty + 3) * DW + (2 * cj + dv - tx + 3)];
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) gs[t][tid] = g[t];
+    }
     __syncthreads();
-    src_load(p, sr, min(tile + (int)gridDim.x, ntiles - 1), true);
-    build_up(p, Y0, X0, src, up);
-    __syncthreads();
-    if (4 * q < p.c) {
-#pragma unroll 2
-      for (int i = 0; i < 8; ++i) {
-        const int pix = pg * 8 + i, py = pix / ST, px = pix % ST;
-        const float g = dyl[pix];
+    if (q < nq) {
+      for (int pix = pg; pix < T * T; pix += NT / NQ) {
+        const int i = i0 + pix / T, j = j0 + pix % T;
+        if (i >= p.h || j >= p.w) continue;
+        float G[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) G[t] = gs[t][pix];
+        const long off = (((long)img * p.h + i) * p.w + j) * p.c + 4 * q;
+        float4 da = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-          const float4 v = *reinterpret_cast<const float4*>(
-              up + ((py + t / 3) * UT + px + t % 3) * CS + 4 * q);
-          acc[t].x += v.x * g;
-          acc[t].y += v.y * g;
-          acc[t].z += v.z * g;
-          acc[t].w += v.w * g;
+          da.x += wv[t].x * G[t];
+          da.y += wv[t].y * G[t];
+          da.z += wv[t].z * G[t];
+          da.w += wv[t].w * G[t];
+        }
+        if (p.dact) *reinterpret_cast<float4*>(p.dact + off) = da;
+        if (!with_x) continue;
+        const float4 xv = *reinterpret_cast<const float4*>(p.x + off);
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        const float mus[4] = {mu.x, mu.y, mu.z, mu.w}, iss[4] = {is.x, is.y, is.z, is.w};
+        const float gas[4] = {ga.x, ga.y, ga.z, ga.w}, bes[4] = {be.x, be.y, be.z, be.w};
+        const float das[4] = {da.x, da.y, da.z, da.w};
+        float a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float xh = (xs[u] - mus[u]) * iss[u];
+          const float z = xh * gas[u] + bes[u];
+          a[u] = act_fwd(ACT_RELU, z);
+          const float dz = das[u] * act_grad(ACT_RELU, z);
+          s0[u] += (double)dz;
+          s1[u] += (double)dz * (double)xh;
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          dwacc[t].x += a[0] * G[t];
+          dwacc[t].y += a[1] * G[t];
+          dwacc[t].z += a[2] * G[t];
+          dwacc[t].w += a[3] * G[t];
         }
       }
     }
   }
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+
+  // workgroup reduction (fixed order): the 8 pixel groups of a wave by butterfly, then the waves
+  const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int o = 8; o < 64; o <<= 1) {
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {
-      acc[t].x += __shfl_xor(acc[t].x, o);
-      acc[t].y += __shfl_xor(acc[t].y, o);
-      acc[t].z += __shfl_xor(acc[t].z, o);
-      acc[t].w += __shfl_xor(acc[t].w, o);
+    for (int t = 0; t < 9; ++t) {
+      dwacc[t].x += __shfl_xor(dwacc[t].x, o);
+      dwacc[t].y += __shfl_xor(dwacc[t].y, o);
+      dwacc[t].z += __shfl_xor(dwacc[t].z, o);
+      dwacc[t].w += __shfl_xor(dwacc[t].w, o);
     }
-  if (lane < 8 && 4 * lane < p.c) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
-      *reinterpret_cast<float4*>(&comb[wave][t * CMAX + 4 * lane]) = acc[t];
+    for (int u = 0; u < 4; ++u) {
+      s0[u] += __shfl_xor(s0[u], o);
+      s1[u] += __shfl_xor(s1[u], o);
+    }
+  }
+  if (lane < NQ) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) comb[wave][t][lane] = dwacc[t];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bcomb[wave][0][4 * lane + u] = s0[u];
+      bcomb[wave][1][4 * lane + u] = s1[u];
+    }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 9 * p.c; e += NT) {
-    const int t = e / p.c, c = e - t * p.c;
-    const int o = t * CMAX + c;
-    p.part[(long)blockIdx.x * 9 * p.c + e] = ((comb[0][o] + comb[1][o]) + comb[2][o]) + comb[3][o];
+  if (p.dwpart && with_x) {
+    for (int e = tid; e < 9 * p.c; e += NT) {
+      const int t = e / p.c, c = e - t * p.c;
+      const float* c0 = reinterpret_cast<const float*>(&comb[0][t][0]) + c;
+      const float* c1 = reinterpret_cast<const float*>(&comb[1][t][0]) + c;
+      const float* c2 = reinterpret_cast<const float*>(&comb[2][t][0]) + c;
+      const float* c3 = reinterpret_cast<const float*>(&comb[3][t][0]) + c;
+      p.dwpart[(long)e * gridDim.x + blockIdx.x] = ((*c0 + *c1) + *c2) + *c3;
+    }
+  }
+  if (p.bnpart && with_x && tid < p.c) {
+    const double a0 = ((bcomb[0][0][tid] + bcomb[1][0][tid]) + bcomb[2][0][tid]) + bcomb[3][0][tid];
+    const double a1 = ((bcomb[0][1][tid] + bcomb[1][1][tid]) + bcomb[2][1][tid]) + bcomb[3][1][tid];
+    *reinterpret_cast<double2*>(p.bnpart + ((long)tid * gridDim.x + blockIdx.x) * 2) =
+        make_double2(a0, a1);
   }
 }
 
-__global__ __launch_bounds__(256) void upconv_wgrad_reduce_kernel(const float* __restrict__ part,
-                                                                  int nb, int per,
-                                                                  float* __restrict__ dw) {
+// dw[e] = sum over the workgroups' partial rows, in order (fp64), e = t c + channel (HWIO)
+__global__ __launch_bounds__(256) void upconv_dw_reduce_kernel(const float* __restrict__ part,
+                                                               int nb, float* __restrict__ dw) {
   __shared__ double red[256];
   const int e = blockIdx.x;
   double s = 0.0;
-  for (int b = threadIdx.x; b < nb; b += 256) s += part[(long)b * per + e];
+  for (int b = threadIdx.x; b < nb; b += 256) s += part[(long)e * nb + b];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -272,80 +363,8 @@ __global__ __launch_bounds__(256) void upconv_wgrad_reduce_kernel(const float* _
   if (threadIdx.x == 0) dw[e] = (float)red[0];
 }
 
-// one workgroup per DT x DT source tile: the DU x DU window of the 2x-map gradient
-// dup[q][c] = sum_t w[t][c] dy[q - t + 1] (zero outside the 2x map) in LDS, then each source
-// pixel gathers its bilinear adjoint: the 2x rows u in 2i-1 .. 2i+2 whose lerp taps land on i,
-// weight (1 - l) for the lower tap and l for the upper (both, at a clamped border).
-__global__ __launch_bounds__(NT) void upconv_dgrad_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) float dup[DU * DU * CS];
-  __shared__ float dyl[DY * DY];
-  __shared__ __attribute__((aligned(16))) float wl[9 * CMAX];
-  const int H2 = 2 * p.h, W2 = 2 * p.w, nq = p.c / 4;
-  const int j0 = blockIdx.x * DT, i0 = blockIdx.y * DT, img = blockIdx.z;
-  const int u0 = 2 * i0 - 1, v0 = 2 * j0 - 1;  // dup window origin
-  for (int e = threadIdx.x; e < 9 * p.c; e += NT) wl[(e / p.c) * CMAX + e % p.c] = p.wt[e];
-  // dy window: dyl[a][b] = dy[u0 - 1 + a][v0 - 1 + b]
-  for (int e = threadIdx.x; e < DY * DY; e += NT) {
-    const int yy = u0 - 1 + e / DY, xx = v0 - 1 + e % DY;
-    dyl[e] = (yy >= 0 && yy < H2 && xx >= 0 && xx < W2) ? p.dy[((long)img * H2 + yy) * W2 + xx]
-                                                         : 0.f;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < DU * DU * nq; e += NT) {
-    const int q = e % nq, pix = e / nq;
-    const int a = pix / DU, b = pix % DU;
-    const int uy = u0 + a, ux = v0 + b;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (uy >= 0 && uy < H2 && ux >= 0 && ux < W2) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        // y[p] = sum_t w[t] up[p + t - 1]  =>  dup[q] = sum_t w[t] dy[q - t + 1]
-        const float g = dyl[(a + 2 - t / 3) * DY + b + 2 - t % 3];
-        const float4 f = *reinterpret_cast<const float4*>(wl + t * CMAX + 4 * q);
-        o.x += g * f.x; o.y += g * f.y; o.z += g * f.z; o.w += g * f.w;
-      }
-    }
-    *reinterpret_cast<float4*>(dup + pix * CS + 4 * q) = o;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < DT * DT * nq; e += NT) {
-    const int q = e % nq, pix = e / nq;
-    const int i = i0 + pix / DT, j = j0 + pix % DT;
-    if (i >= p.h || j >= p.w) continue;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int du = -1; du <= 2; ++du) {
-      const int uy = 2 * i + du;
-      if (uy < 0 || uy >= H2) continue;
-      int y0, y1;
-      float yl;
-      lerp_coords(uy, p.h, y0, y1, yl);
-      const float wy = (y0 == i ? 1.f - yl : 0.f) + (y1 == i ? yl : 0.f);
-      if (wy == 0.f) continue;
-#pragma unroll
-      for (int dv = -1; dv <= 2; ++dv) {
-        const int ux = 2 * j + dv;
-        if (ux < 0 || ux >= W2) continue;
-        int x0, x1;
-        float xl;
-        lerp_coords(ux, p.w, x0, x1, xl);
-        const float wx = (x0 == j ? 1.f - xl : 0.f) + (x1 == j ? xl : 0.f);
-        if (wx == 0.f) continue;
-        const float ww = wy * wx;
-        const float4 g = *reinterpret_cast<const float4*>(
-            dup + ((uy - u0) * DU + (ux - v0)) * CS + 4 * q);
-        a.x += ww * g.x; a.y += ww * g.y; a.z += ww * g.z; a.w += ww * g.w;
-      }
-    }
-    *reinterpret_cast<float4*>(p.y + (((long)img * p.h + i) * p.w + j) * p.c + 4 * q) = a;
-  }
-}
-
-constexpr int FWD_BLOCKS = 2048;
-constexpr int WG_BLOCKS = 2048;
-
 static bool args_ok(const float* x, int n, int h, int w, int c) {
-  return x && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && c <= CMAX && aligned16(x);
+  return x && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && c <= CM && aligned16(x);
 }
 
 static Params mk(const float* x, int n, int h, int w, int c, const float* mean,
@@ -354,18 +373,33 @@ static Params mk(const float* x, int n, int h, int w, int c, const float* mean,
   p.x = x;
   p.n = n; p.h = h; p.w = w; p.c = c;
   p.mean = mean; p.invstd = invstd; p.gamma = gamma; p.beta = beta;
-  p.tiles_x = (int)cdiv(2 * w, ST);
-  p.tiles_y = (int)cdiv(2 * h, ST);
+  p.tiles_x = (int)cdiv(w, T);
+  p.tiles_y = (int)cdiv(h, T);
   return p;
 }
+
+static size_t dw_bytes(int c) { return ((sizeof(float) * (size_t)BWD_BLOCKS * 9 * c) + 255) / 256 * 256; }
+static size_t bn_bytes(int c) { return sizeof(double) * 2 * (size_t)BWD_BLOCKS * c; }
 
 }  // namespace upc
 }  // namespace pld
 
 using namespace pld;
 
+// bn.hip: finalize (dgamma, dbeta, k1, k2 from channel-major partials) + apply
+extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
+                                  int64_t rows, int c, const float* mean, const float* invstd,
+                                  const float* gamma, const float* beta, int act, float* dx,
+                                  int dx_accumulate, float* dgamma, float* dbeta,
+                                  int param_accumulate, float* k12, hipStream_t st);
+
+extern "C" size_t pld_upconv_bwd_workspace_size(int c) {
+  if (c <= 0) return 0;
+  return upc::dw_bytes(c) + upc::bn_bytes(c) + 2 * sizeof(float) * (size_t)c + 64;
+}
+
 extern "C" size_t pld_upconv_wgrad_workspace_size(int c) {
-  return c > 0 ? sizeof(float) * (size_t)upc::WG_BLOCKS * 9 * c : 0;
+  return pld_upconv_bwd_workspace_size(c);
 }
 
 extern "C" int pld_upconv_fwd(const float* x, int n, int h, int w, int c, const float* mean,
@@ -373,47 +407,75 @@ extern "C" int pld_upconv_fwd(const float* x, int n, int h, int w, int c, const 
                               const float* wt, const float* bias, float* y, void* stream) {
   PLD_CHECK_ARG(upc::args_ok(x, n, h, w, c) && mean && invstd && gamma && beta && wt && y,
                 "pld_upconv_fwd: bad args (c %% 4 == 0, c <= 32, 16-byte aligned x)");
+  PLD_CHECK_ARG(aligned16(mean) && aligned16(invstd) && aligned16(gamma) && aligned16(beta),
+                "pld_upconv_fwd: BN parameters must be 16-byte aligned");
   upc::Params p = upc::mk(x, n, h, w, c, mean, invstd, gamma, beta);
   p.wt = wt;
   p.bias = bias;
   p.y = y;
   const int ntiles = p.tiles_x * p.tiles_y * n;
-  upc::upconv_fwd_kernel<<<std::min(upc::FWD_BLOCKS, ntiles), upc::NT, 0, as_stream(stream)>>>(p);
+  upc::upconv_fwd_kernel<<<ntiles, upc::NT, 0, as_stream(stream)>>>(p);
   return check_launch("upconv_fwd_kernel");
+}
+
+extern "C" int pld_upconv_bwd(const float* x, int n, int h, int w, int c, const float* mean,
+                              const float* invstd, const float* gamma, const float* beta,
+                              const float* wt, const float* dy, float* dact, float* dw, float* dx,
+                              int dx_accumulate, float* dgamma, float* dbeta,
+                              int param_accumulate, void* ws, size_t ws_bytes, void* stream) {
+  PLD_CHECK_ARG(dy && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && c <= upc::CM,
+                "pld_upconv_bwd: bad args (c %% 4 == 0, c <= 32)");
+  PLD_CHECK_ARG(wt || !dact, "pld_upconv_bwd: dact needs the filter wt");
+  PLD_CHECK_ARG(!dact || aligned16(dact), "pld_upconv_bwd: dact must be 16-byte aligned");
+  PLD_CHECK_ARG(!dx || dact, "pld_upconv_bwd: the BN backward (dx) needs the dact buffer");
+  PLD_CHECK_ARG(!dx || (dgamma && dbeta), "pld_upconv_bwd: dx needs dgamma and dbeta");
+  const bool need_x = dw || dx;
+  PLD_CHECK_ARG(!need_x || (upc::args_ok(x, n, h, w, c) && mean && invstd && gamma && beta &&
+                            aligned16(mean) && aligned16(invstd) && aligned16(gamma) &&
+                            aligned16(beta)),
+                "pld_upconv_bwd: dw / dx need x and 16-byte aligned BN parameters");
+  PLD_CHECK_ARG(!need_x || (ws && ws_bytes >= pld_upconv_bwd_workspace_size(c)),
+                "pld_upconv_bwd: workspace too small");
+  upc::Params p = upc::mk(need_x ? x : nullptr, n, h, w, c, mean, invstd, gamma, beta);
+  p.wt = wt;
+  p.dy = dy;
+  p.dact = dact;
+  char* wsb = (char*)ws;
+  p.dwpart = dw ? (float*)wsb : nullptr;
+  p.bnpart = dx ? (double*)(wsb + upc::dw_bytes(c)) : nullptr;
+  const int ntiles = p.tiles_x * p.tiles_y * n;
+  const int nb = std::min(upc::BWD_BLOCKS, ntiles);
+  hipStream_t st = as_stream(stream);
+  upc::upconv_bwd_kernel<<<nb, upc::NT, 0, st>>>(p);
+  int rc = check_launch("upconv_bwd_kernel");
+  if (rc) return rc;
+  if (dw) {
+    upc::upconv_dw_reduce_kernel<<<9 * c, 256, 0, st>>>(p.dwpart, nb, dw);
+    rc = check_launch("upconv_dw_reduce_kernel");
+    if (rc) return rc;
+  }
+  if (dx) {
+    float* k12 = (float*)(wsb + upc::dw_bytes(c) + upc::bn_bytes(c));
+    rc = pld__bn_bwd_finish(p.bnpart, nb, x, dact, (int64_t)n * h * w, c, mean, invstd, gamma,
+                            beta, ACT_RELU, dx, dx_accumulate, dgamma, dbeta, param_accumulate,
+                            k12, st);
+  }
+  return rc;
 }
 
 extern "C" int pld_upconv_wgrad(const float* x, int n, int h, int w, int c, const float* mean,
                                 const float* invstd, const float* gamma, const float* beta,
                                 const float* dy, float* dw, void* ws, size_t ws_bytes,
                                 void* stream) {
-  PLD_CHECK_ARG(upc::args_ok(x, n, h, w, c) && mean && invstd && gamma && beta && dy && dw,
-                "pld_upconv_wgrad: bad args");
-  PLD_CHECK_ARG(ws && ws_bytes >= pld_upconv_wgrad_workspace_size(c),
-                "pld_upconv_wgrad: workspace too small");
-  upc::Params p = upc::mk(x, n, h, w, c, mean, invstd, gamma, beta);
-  p.dy = dy;
-  p.part = (float*)ws;
-  const int ntiles = p.tiles_x * p.tiles_y * n;
-  const int nb = std::min(upc::WG_BLOCKS, ntiles);
-  hipStream_t st = as_stream(stream);
-  upc::upconv_wgrad_kernel<<<nb, upc::NT, 0, st>>>(p);
-  int rc = check_launch("upconv_wgrad_kernel");
-  if (rc) return rc;
-  upc::upconv_wgrad_reduce_kernel<<<9 * c, 256, 0, st>>>(p.part, nb, 9 * c, dw);
-  return check_launch("upconv_wgrad_reduce_kernel");
+  PLD_CHECK_ARG(dw, "pld_upconv_wgrad: dw is NULL");
+  // no filter taps needed: they only enter dact, which is not formed here
+  return pld_upconv_bwd(x, n, h, w, c, mean, invstd, gamma, beta, nullptr, dy, nullptr, dw,
+                        nullptr, 0, nullptr, nullptr, 0, ws, ws_bytes, stream);
 }
 
 extern "C" int pld_upconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wt,
                                 float* dact, void* stream) {
-  PLD_CHECK_ARG(dy && wt && dact && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 &&
-                    c <= upc::CMAX && aligned16(dact),
-                "pld_upconv_dgrad: bad args");
-  upc::Params p{};
-  p.dy = dy;
-  p.wt = wt;
-  p.y = dact;
-  p.n = n; p.h = h; p.w = w; p.c = c;
-  dim3 grid(cdiv(w, upc::DT), cdiv(h, upc::DT), n);
-  upc::upconv_dgrad_kernel<<<grid, upc::NT, 0, as_stream(stream)>>>(p);
-  return check_launch("upconv_dgrad_kernel");
+  PLD_CHECK_ARG(dact, "pld_upconv_dgrad: dact is NULL");
+  return pld_upconv_bwd(nullptr, n, h, w, c, nullptr, nullptr, nullptr, nullptr, wt, dy, dact,
+                        nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, 0, stream);
 }

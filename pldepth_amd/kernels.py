@@ -531,6 +531,21 @@ def upconv_wgrad(x, bn, dy, dw):
                            ptr(dy), ptr(dw), ptr(ws), need, stream())
 
 
+def upconv_bwd(x, bn, wt, dy, dact, dw=None, dx=None, dgamma=None, dbeta=None,
+               dx_accumulate=False, param_accumulate=False):
+    """The fused last stage's backward in one pass over (x, dy): dact [n,h,w,c] (gradient of
+    relu(bn(x))), dw [3,3,c,1] if given, and if dx is given the BN + ReLU backward of x
+    (dx, dgamma, dbeta) with its channel reductions taken in the same pass."""
+    n, h, w, c = x.shape
+    mean, invstd, gamma, beta = bn
+    need = lib().pld_upconv_bwd_workspace_size(c)
+    ws = workspace(need, "upconv")
+    lib().pld_upconv_bwd(ptr(x), n, h, w, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                         ptr(wt), ptr(dy), ptr(dact), ptr(dw), ptr(dx), int(dx_accumulate),
+                         ptr(dgamma), ptr(dbeta), int(param_accumulate), ptr(ws), need,
+                         stream())
+
+
 def upconv_dgrad(dy, wt, dact):
     """dact [n,h,w,c] = up2x^T(conv3x3^T(dy)) for dy [n,2h,2w,1], wt [3,3,c,1] (HWIO)."""
     n, h, w, c = dact.shape

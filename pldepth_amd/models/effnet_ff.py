@@ -444,12 +444,15 @@ class EffNetFF:
         # final conv (bias, no BN)
         last = len(self.dec) - 1
         if self.fuse_final:
-            # through the fused upsample: dec4's activation gradient straight from dpred
+            # through the fused upsample, one pass over (dec4_pre, dpred): the filter gradient,
+            # dec4's activation gradient and the whole dec_bn4 + ReLU backward (its channel
+            # reductions accumulated in the same pass) into dec4's pre-BN gradient
             _, bn4, _ = self.dec[last]
-            K.upconv_wgrad(A["dec4_pre"], (bn4.mean, bn4.invstd, bn4.gamma, bn4.beta), dpred,
-                           self.final.dw)
+            gpre4 = self._gpre_buf(A[f"dec{last}_pre"].shape)
+            K.upconv_bwd(A["dec4_pre"], (bn4.mean, bn4.invstd, bn4.gamma, bn4.beta),
+                         self.final.w_nat, dpred, G[f"dec{last}_act"], dw=self.final.dw,
+                         dx=gpre4, dgamma=bn4.dgamma, dbeta=bn4.dbeta)
             K.channel_sum(dpred, B * h * w, 1, self.final.db)
-            K.upconv_dgrad(dpred, self.final.w_nat, G[f"dec{last}_act"])
         else:
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
@@ -468,7 +471,8 @@ class EffNetFF:
                 K.upsample2x_bwd(G[f"dec{i}_up"], G[f"dec{i}_act"])
             rows = B * h * w
             gpre = self._gpre_buf(A[f"dec{i}_pre"].shape)
-            bn.bwd(A[f"dec{i}_pre"], G[f"dec{i}_act"], rows, "relu", gpre)
+            if not (i == last and self.fuse_final):  # (fused: done by upconv_bwd above)
+                bn.bwd(A[f"dec{i}_pre"], G[f"dec{i}_act"], rows, "relu", gpre)
             if i == 0:
                 x1, x2, g1, g2 = A["top_activation"], None, G["top_activation"], None
             else:

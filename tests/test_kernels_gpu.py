@@ -791,8 +791,9 @@ def test_thin_1x1_conv(cuda, n, h, w, cin, cout):
 @pytest.mark.parametrize("n,h,w,c", [(2, 5, 7, 8), (1, 16, 16, 32), (2, 33, 20, 32),
                                      (2, 224, 224, 32)])
 def test_upconv_matches_unfused_path(cuda, n, h, w, c):
-    """pld_upconv_{fwd,wgrad,dgrad} (csrc/upconv.hip) against the unfused kernels they replace:
-    pld_upsample2x_fwd_bn + pld_conv2d_fwd / _wgrad / _dgrad + pld_upsample2x_bwd."""
+    """pld_upconv_{fwd,wgrad,dgrad,bwd} (csrc/upconv.hip: the 9 tap maps at 1x resolution)
+    against the unfused kernels they replace: pld_upsample2x_fwd_bn + pld_conv2d_fwd / _wgrad /
+    _dgrad + pld_upsample2x_bwd, then pld_bn_bwd (relu) for the fused BN backward."""
     g = torch.Generator(device=cuda).manual_seed(n * h + w)
     x = torch.randn(n, h, w, c, device=cuda, generator=g)
     mean = torch.randn(c, device=cuda, generator=g) * 0.1
@@ -823,10 +824,21 @@ def test_upconv_matches_unfused_path(cuda, n, h, w, c):
     K.upconv_wgrad(x, bn, dy, dw)
     dact = torch.empty_like(x)
     K.upconv_dgrad(dy, wt, dact)
+    # the one-pass backward with the BN + ReLU backward folded in
+    dact2, dw2, dx2 = torch.empty_like(x), torch.empty_like(wt), torch.empty_like(x)
+    dg2, db2 = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.upconv_bwd(x, bn, wn, dy, dact2, dw=dw2, dx=dx2, dgamma=dg2, dbeta=db2)
+    dx_ref = torch.empty_like(x)
+    dg_ref, db_ref = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd(x, dact_ref, n * h * w, c, mean, invstd, gamma, beta, "relu", dx_ref, dg_ref,
+             db_ref)
     torch.cuda.synchronize()
-    assert rel_err(y, y_ref) < 1e-6
+    assert rel_err(y, y_ref) < 1e-5
     assert rel_err(dw, dw_ref) < 1e-5
     assert rel_err(dact, dact_ref) < 1e-5
+    assert torch.equal(dact2, dact) and torch.equal(dw2, dw)
+    assert rel_err(dx2, dx_ref) < 1e-4, rel_err(dx2, dx_ref)
+    assert rel_err(dg2, dg_ref) < 1e-5 and rel_err(db2, db_ref) < 1e-5
     # and against torch-CPU fp64 for the whole composition
     x64 = x.double().cpu().permute(0, 3, 1, 2)
     a = torch.relu((x64 - mean.double().cpu().view(1, -1, 1, 1)) *
