@@ -339,6 +339,21 @@ int pld_se_bwd_bn(const float* dy, const float* x, const float* mean, const floa
                   const float* gamma, const float* beta, int act, int n, int hw, int c, int cse,
                   const float* w1, const float* w2, const float* z1, const float* gate,
                   float* addn, void* ws, void* stream);
+/* pld_se_bwd_bn + the block's BatchNormalization + activation backward in one sweep
+ * (pl_hourglass.py:52-57 via Keras EfficientNet block: bn -> swish -> SE -> project): the SE
+ * squeeze over (x, dy) also gathers per (image, channel) sum dy act'(z), sum act'(z) and their
+ * xhat-weighted sums, from which, once addn is known, the BN's reductions follow exactly
+ * (dz = (dy gate + addn) act'(z) is affine in the per-image constants gate, addn); then
+ * dx (=|+=) the pre-BN gradient as pld_bn_bwd(x, dy, ..., gate, addn) computes it, and
+ * dgamma/dbeta (=|+= by param_accumulate). Replaces pld_se_bwd_bn + pld_bn_bwd (one fewer pass
+ * over x and dy). Workspace: pld_se_bwd_bn_full_workspace_size. */
+size_t pld_se_bwd_bn_full_workspace_size(int n, int hw, int c, int cse);
+int pld_se_bwd_bn_full(const float* dy, const float* x, const float* mean, const float* invstd,
+                       const float* gamma, const float* beta, int act, int n, int hw, int c,
+                       int cse, const float* w1, const float* w2, const float* z1,
+                       const float* gate, float* addn, float* dx, int dx_accumulate,
+                       float* dgamma, float* dbeta, int param_accumulate, void* ws,
+                       size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Ranking sampler (pldepth/data/sampling.py), split into draws and a deterministic part.

@@ -94,6 +94,9 @@ _SIGS = {
     "pld_se_bwd": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P]),
     "pld_se_fwd_bn": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
     "pld_se_bwd_bn": (I32, [P, P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, P]),
+    "pld_se_bwd_bn_full_workspace_size": (SZ, [I32, I32, I32, I32]),
+    "pld_se_bwd_bn_full": (I32, [P, P, P, P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P, I32,
+                                 P, P, I32, P, SZ, P]),
     "pld_sampler_workspace_size": (SZ, [I32, I32, I32, I32, I32, I32]),
     "pld_sampler_compact": (I32, [P, I32, I32, I32, P, P, P, P, P, P]),
     "pld_sampler_compact_workspace_size": (SZ, [I32, I32, I32]),
@@ -118,7 +121,7 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",
-               "pld_upconv_bwd_workspace_size"}
+               "pld_upconv_bwd_workspace_size", "pld_se_bwd_bn_full_workspace_size"}
 
 
 def declared_symbols(header=HEADER):

@@ -665,15 +665,17 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
 // internal (upconv.hip): the BN backward from partials a producer kernel accumulated
 extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
                                   int64_t rows, int c, const float* mean, const float* invstd,
-                                  const float* gamma, const float* beta, int act, float* dx,
+                                  const float* gamma, const float* beta, int act,
+                                  const float* gate, const float* addn, int hw, float* dx,
                                   int dx_accumulate, float* dgamma, float* dbeta,
                                   int param_accumulate, float* k12, hipStream_t st) {
   PLD_CHECK_ARG(part && x && dy && mean && invstd && gamma && beta && k12 && rows > 0 && c > 0,
                 "pld__bn_bwd_finish: bad args");
   PLD_CHECK_ARG(rows * c < (1L << 31), "pld__bn_bwd_finish: tensor too large");
-  return bn_bwd_finish(part, nparts, x, dy, rows, c, mean, invstd, gamma, beta, act, nullptr,
-                       nullptr, FastDiv(1), nullptr, dx, dx_accumulate, nullptr, 0, dgamma, dbeta,
-                       param_accumulate, k12, st);
+  PLD_CHECK_ARG(!(gate || addn) || hw > 0, "pld__bn_bwd_finish: gate/addn need hw > 0");
+  return bn_bwd_finish(part, nparts, x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn,
+                       FastDiv((uint32_t)std::max(hw, 1)), nullptr, dx, dx_accumulate, nullptr, 0,
+                       dgamma, dbeta, param_accumulate, k12, st);
 }
 
 extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,

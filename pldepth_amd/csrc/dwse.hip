@@ -288,12 +288,19 @@ __device__ __forceinline__ float4 se_pro(const SePro& pr, float4 v, float4 mu, f
 }
 
 // per-image channel sums of a (or of a*dy): partial[img][split][c] (fp64); 4 rows of loads in
-// flight per thread (the same summation order as one row at a time)
-template <bool PRO>
+// flight per thread (the same summation order as one row at a time).
+// BNB (backward, with the BN + activation prologue): also the four per-(image, channel) sums
+// from which the block BN's backward reductions follow once the SE has produced addn:
+//   A1 = sum dy act'(z), A2 = sum act'(z), B1 = sum dy act'(z) xhat, B2 = sum act'(z) xhat,
+// so that sum dz = gate A1 + addn A2 and sum dz xhat = gate B1 + addn B2 for
+// dz = (dy gate + addn) act'(z) (chan_reduce's RED_BNBWD with gate / addn): part4[k][img][split][c].
+template <bool PRO, bool BNB = false>
 __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restrict__ a,
                                                            const float* __restrict__ b, int hw,
                                                            int c, int rsplit, SePro pr,
-                                                           double* __restrict__ part) {
+                                                           double* __restrict__ part,
+                                                           double* __restrict__ part4 = nullptr) {
+  static_assert(!BNB || PRO, "the BN-backward sums need the BN prologue");
   const int img = blockIdx.x / rsplit;
   const int sp = blockIdx.x % rsplit;
   const int cv = c / 4;
@@ -306,6 +313,11 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
   const int rows_per = (hw + rsplit - 1) / rsplit;
   const int rb = sp * rows_per, re = min(hw, rb + rows_per);
   double s[4] = {0.0, 0.0, 0.0, 0.0};
+  double bs[4][4];  // [A1, A2, B1, B2][channel]
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bs[k][u] = 0.0;
   if (r0 < rpi) {
     const long base = (long)img * hw * c + 4 * q;
     float4 mu, is, ga, be;
@@ -316,6 +328,24 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
       be = *reinterpret_cast<const float4*>(pr.beta + 4 * q);
     }
     auto acc1 = [&](float4 v, float4 u) {
+      if constexpr (BNB) {
+        const float xs[4] = {v.x, v.y, v.z, v.w}, us[4] = {u.x, u.y, u.z, u.w};
+        const float mus[4] = {mu.x, mu.y, mu.z, mu.w}, iss[4] = {is.x, is.y, is.z, is.w};
+        const float gas[4] = {ga.x, ga.y, ga.z, ga.w}, bes[4] = {be.x, be.y, be.z, be.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xs[e] - mus[e]) * iss[e];
+          const float z = xh * gas[e] + bes[e];
+          const float av = act_fwd(pr.act, z), ag = act_grad(pr.act, z);
+          const float dg = us[e] * ag;
+          s[e] += (double)(av * us[e]);
+          bs[0][e] += (double)dg;
+          bs[1][e] += (double)ag;
+          bs[2][e] += (double)dg * (double)xh;
+          bs[3][e] += (double)ag * (double)xh;
+        }
+        return;
+      }
       if (PRO) v = se_pro(pr, v, mu, is, ga, be);
       if (b) {
         s[0] += (double)(v.x * u.x); s[1] += (double)(v.y * u.y);
@@ -364,6 +394,25 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
     double* o = part + ((long)img * rsplit + sp) * c + 4 * q;
 #pragma unroll
     for (int u = 0; u < 4; ++u) o[u] = s[u];
+  }
+  if constexpr (BNB) {
+    const long plane = (long)gridDim.x * c;  // one [img][split][c] plane per sum
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) red[tid][u] = bs[k][u];
+      __syncthreads();
+      if (r0 == 0 && r0 < rpi) {
+        double t[4] = {bs[k][0], bs[k][1], bs[k][2], bs[k][3]};
+        for (int j = 1; j < rpi; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) t[u] += red[tid + j * ncv][u];
+        double* o = part4 + k * plane + ((long)img * rsplit + sp) * c + 4 * q;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = t[u];
+      }
+    }
   }
 }
 
@@ -483,7 +532,9 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
                                                                const float* __restrict__ w2,
                                                                const float* __restrict__ z1,
                                                                const float* __restrict__ gate,
-                                                               float* __restrict__ addn) {
+                                                               float* __restrict__ addn,
+                                                               const double* __restrict__ part4,
+                                                               double* __restrict__ bnpart) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dz2 = sm;       // [c]
   float* dz1 = sm + c;   // [cse]
@@ -509,7 +560,21 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
     float acc = 0.f;
 #pragma unroll 8
     for (int j = 0; j < cse; ++j) acc += dz1[j] * w1[(long)ch * cse + j];
-    addn[(long)img * c + ch] = acc / (float)hw;
+    const float ad = acc / (float)hw;
+    addn[(long)img * c + ch] = ad;
+    if (bnpart) {
+      // the block BN's backward partials of this image: sum dz = g A1 + addn A2, sum dz xhat =
+      // g B1 + addn B2 per squeeze split -> [ch][img * rsplit + k][2] (bnbwd_finalize's layout)
+      const double g = gate[(long)img * c + ch];
+      const long plane = (long)gridDim.x * rsplit * c, nparts = (long)gridDim.x * rsplit;
+      for (int k = 0; k < rsplit; ++k) {
+        const long o = ((long)img * rsplit + k) * c + ch;
+        const double d0 = g * part4[o] + (double)ad * part4[plane + o];
+        const double d1 = g * part4[2 * plane + o] + (double)ad * part4[3 * plane + o];
+        *reinterpret_cast<double2*>(bnpart + ((long)ch * nparts + (long)img * rsplit + k) * 2) =
+            make_double2(d0, d1);
+      }
+    }
   }
 }
 
@@ -674,7 +739,7 @@ static int se_bwd_impl(const float* dy, const float* a, const SePro& pr, int n, 
   int rc = check_launch("img_chan_sum_kernel(bwd)");
   if (rc) return rc;
   se_fc_bwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse), st>>>(
-      (const double*)ws, rs, hw, c, cse, w1, w2, z1, gate, addn);
+      (const double*)ws, rs, hw, c, cse, w1, w2, z1, gate, addn, nullptr, nullptr);
   return check_launch("se_fc_bwd_kernel");
 }
 
@@ -692,4 +757,57 @@ extern "C" int pld_se_bwd_bn(const float* dy, const float* x, const float* mean,
   PLD_CHECK_ARG(mean && invstd && gamma && beta, "pld_se_bwd_bn: incomplete BN prologue");
   return se_bwd_impl(dy, x, SePro{mean, invstd, gamma, beta, act}, n, hw, c, cse, w1, w2, z1,
                      gate, addn, ws, stream);
+}
+
+// bn.hip: finalize (dgamma, dbeta, k1, k2 from channel-major partials) + apply
+extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
+                                  int64_t rows, int c, const float* mean, const float* invstd,
+                                  const float* gamma, const float* beta, int act,
+                                  const float* gate, const float* addn, int hw, float* dx,
+                                  int dx_accumulate, float* dgamma, float* dbeta,
+                                  int param_accumulate, float* k12, hipStream_t st);
+
+static size_t se_bn_ws_parts(int n, int hw, int c) {
+  return (size_t)n * se_rsplit(n, hw, c) * c;  // doubles per [img][split][c] plane
+}
+
+extern "C" size_t pld_se_bwd_bn_full_workspace_size(int n, int hw, int c, int cse) {
+  if (n <= 0 || hw <= 0 || c <= 0) return 0;
+  // S plane, the 4 BN-sum planes, the [c][parts][2] BN partials, k1 / k2
+  return sizeof(double) * se_bn_ws_parts(n, hw, c) * 7 + 2 * sizeof(float) * (size_t)c + 64;
+}
+
+extern "C" int pld_se_bwd_bn_full(const float* dy, const float* x, const float* mean,
+                                  const float* invstd, const float* gamma, const float* beta,
+                                  int act, int n, int hw, int c, int cse, const float* w1,
+                                  const float* w2, const float* z1, const float* gate,
+                                  float* addn, float* dx, int dx_accumulate, float* dgamma,
+                                  float* dbeta, int param_accumulate, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  PLD_CHECK_ARG(dy && x && mean && invstd && gamma && beta && w1 && w2 && z1 && gate && addn &&
+                    dx && dgamma && dbeta && ws && n > 0 && hw > 0 && c > 0 && cse > 0,
+                "pld_se_bwd_bn_full: bad args");
+  PLD_CHECK_ARG(c % 4 == 0, "pld_se_bwd_bn_full: channels must be a multiple of 4");
+  PLD_CHECK_ARG((long)n * hw * c < (1L << 31), "pld_se_bwd_bn_full: tensor too large");
+  PLD_CHECK_ARG(ws_bytes >= pld_se_bwd_bn_full_workspace_size(n, hw, c, cse),
+                "pld_se_bwd_bn_full: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int rs = se_rsplit(n, hw, c);
+  const size_t np = se_bn_ws_parts(n, hw, c);
+  double* part = (double*)ws;
+  double* part4 = part + np;
+  double* bnpart = part4 + 4 * np;
+  float* k12 = (float*)(bnpart + 2 * np);
+  const SePro pr{mean, invstd, gamma, beta, act};
+  dim3 g1(n * rs, cdiv(c / 4, 256));
+  img_chan_sum_kernel<true, true><<<g1, 256, 0, st>>>(x, dy, hw, c, rs, pr, part, part4);
+  int rc = check_launch("img_chan_sum_kernel(bwd, bn)");
+  if (rc) return rc;
+  se_fc_bwd_kernel<<<dim3(n, SE_SLICES), SE_THREADS, sizeof(float) * (c + cse), st>>>(
+      part, rs, hw, c, cse, w1, w2, z1, gate, addn, part4, bnpart);
+  rc = check_launch("se_fc_bwd_kernel");
+  if (rc) return rc;
+  return pld__bn_bwd_finish(bnpart, n * rs, x, dy, (int64_t)n * hw, c, mean, invstd, gamma, beta,
+                            act, gate, addn, hw, dx, dx_accumulate, dgamma, dbeta,
+                            param_accumulate, k12, st);
 }

@@ -389,7 +389,8 @@ using namespace pld;
 // bn.hip: finalize (dgamma, dbeta, k1, k2 from channel-major partials) + apply
 extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
                                   int64_t rows, int c, const float* mean, const float* invstd,
-                                  const float* gamma, const float* beta, int act, float* dx,
+                                  const float* gamma, const float* beta, int act,
+                                  const float* gate, const float* addn, int hw, float* dx,
                                   int dx_accumulate, float* dgamma, float* dbeta,
                                   int param_accumulate, float* k12, hipStream_t st);
 
@@ -457,8 +458,8 @@ extern "C" int pld_upconv_bwd(const float* x, int n, int h, int w, int c, const 
   if (dx) {
     float* k12 = (float*)(wsb + upc::dw_bytes(c) + upc::bn_bytes(c));
     rc = pld__bn_bwd_finish(p.bnpart, nb, x, dact, (int64_t)n * h * w, c, mean, invstd, gamma,
-                            beta, ACT_RELU, dx, dx_accumulate, dgamma, dbeta, param_accumulate,
-                            k12, st);
+                            beta, ACT_RELU, nullptr, nullptr, 0, dx, dx_accumulate, dgamma,
+                            dbeta, param_accumulate, k12, st);
   }
   return rc;
 }

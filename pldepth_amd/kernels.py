@@ -631,6 +631,21 @@ def se_bwd(dy, a, w1, w2, z1, gate, addn, bn=None, act="swish"):
                             ptr(ws), stream())
 
 
+def se_bwd_bn_full(dy, x, bn, w1, w2, z1, gate, addn, dx, dgamma, dbeta, act="swish",
+                   dx_accumulate=False, param_accumulate=False):
+    """SE backward (addn) + the block BN's backward (dx, dgamma, dbeta) with the BN reductions
+    gathered by the SE squeeze sweep over (x, dy): pld_se_bwd_bn_full."""
+    n, h, w, c = x.shape
+    cse = w1.shape[-1]
+    need = lib().pld_se_bwd_bn_full_workspace_size(n, h * w, c, cse)
+    ws = workspace(need, "se_bn")
+    mu, inv, g, b = bn
+    lib().pld_se_bwd_bn_full(ptr(dy), ptr(x), ptr(mu), ptr(inv), ptr(g), ptr(b), ACT[act], n,
+                             h * w, c, cse, ptr(w1), ptr(w2), ptr(z1), ptr(gate), ptr(addn),
+                             ptr(dx), int(dx_accumulate), ptr(dgamma), ptr(dbeta),
+                             int(param_accumulate), ptr(ws), need, stream())
+
+
 # -------------------------------------------------------------------------------- sampler
 def sampler_candidates(R, strategy):
     return lib().pld_sampler_candidates(R, SAMPLER[strategy])

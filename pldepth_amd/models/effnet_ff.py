@@ -526,12 +526,12 @@ class EffNetFF:
                        gp, blk["project"].w_dg, gse)
         F = self.frozen
         bn = blk["bn"]
-        K.se_bwd(gse, A[n + "dw_pre"], F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
-                 F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), blk["z1"], blk["gate"],
-                 blk["addn"], bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="swish")
         gdw = self._gpre_buf(A[n + "dw_pre"].shape)
-        blk["bn"].bwd(A[n + "dw_pre"], gse, rows, "swish", gdw, gate=blk["gate"],
-                      addn=blk["addn"], hw=oh * ow)
+        # SE backward + the block BN's backward; the BN reductions ride on the SE squeeze sweep
+        K.se_bwd_bn_full(gse, A[n + "dw_pre"], (bn.mean, bn.invstd, bn.gamma, bn.beta),
+                         F[blk["se_w1"]].view(blk["cexp"], blk["cse"]),
+                         F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), blk["z1"], blk["gate"],
+                         blk["addn"], gdw, bn.dgamma, bn.dbeta, act="swish")
         pt, pl = blk["pad"]
         if blk["ex"] != 1:
             ge = G[n + "expand_activation"]

@@ -537,6 +537,20 @@ def test_se_with_bn_prologue(cuda, n, h, w, c, cse):
     torch.cuda.synchronize()
     da = gdy * gg.view(n, 1, 1, c) + addn.view(n, 1, 1, c)
     assert rel_err(da, a.grad) < 1e-4
+    # the SE backward with the block BN's backward folded into its squeeze sweep
+    # (pld_se_bwd_bn_full) == pld_se_bwd_bn + pld_bn_bwd(gate, addn)
+    gam_d, bet_d = bn[2], bn[3]
+    dx_ref = torch.empty_like(gx)
+    dg_ref, db_ref = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd(gx, gdy, n * h * w, c, bn[0], bn[1], gam_d, bet_d, "swish", dx_ref, dg_ref, db_ref,
+             gate=gg, addn=addn, hw=h * w)
+    addn2, dx2 = torch.empty_like(addn), torch.empty_like(gx)
+    dg2, db2 = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.se_bwd_bn_full(gdy, gx, bn, W1, W2, gz, gg, addn2, dx2, dg2, db2, act="swish")
+    torch.cuda.synchronize()
+    assert rel_err(addn2, addn) < 1e-6
+    assert rel_err(dg2, dg_ref) < 1e-5 and rel_err(db2, db_ref) < 1e-5
+    assert rel_err(dx2, dx_ref) < 1e-5, rel_err(dx2, dx_ref)
 
 
 # ------------------------------------------------------------------------------- sampler

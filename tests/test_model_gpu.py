@@ -12,7 +12,7 @@ from oracle import listmle as LM
 from pldepth_amd import kernels as K
 from pldepth_amd.models.effnet_ff import EffNetFF
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("fixed_schedules")]
 TOL = 1e-3
 
 
@@ -30,7 +30,7 @@ def make_rankings(rng, B, H, W, R, L):
 
 
 @pytest.fixture(scope="module")
-def step_results(cuda):
+def step_results(cuda, fixed_schedules):
     B, H, R, L = 2, 64, 12, 5
     eng = EffNetFF((H, H, 3), B, seed=0)
     eng.drop_connect = False

@@ -11,7 +11,7 @@ from oracle import redweb as OR
 from pldepth_amd import kernels as K
 from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("fixed_schedules")]
 TOL = 1e-3
 
 
@@ -32,7 +32,7 @@ STRUCTURAL_ZERO = {"aol/conv0/bias", "aol/conv1/bias", "aol/conv2/bias"}
 
 
 @pytest.fixture(scope="module")
-def step_results(cuda):
+def step_results(cuda, fixed_schedules):
     B, H, R, L = 2, 128, 16, 5
     eng = RedWebFF((H, H, 3), B, seed=0)
     rng = np.random.default_rng(1)
