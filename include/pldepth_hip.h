@@ -205,6 +205,33 @@ int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float
                const float* gate, const float* addn, int hw, float* dx, int dx_accumulate,
                float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
 
+/* pld_bn_bwd's channel reductions + finalize only: dgamma/dbeta (=|+=) and k12 [2][c] =
+ * [mean(dz) | mean(dz xhat)], for a consumer that forms dx on the fly (pld_pgemm_bn_bwd).
+ * Workspace as pld_bn_bwd. */
+int pld_bn_bwd_coeffs(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                      const float* invstd, const float* gamma, const float* beta, int act,
+                      float* dgamma, float* dbeta, int param_accumulate, float* k12, void* ws,
+                      void* stream);
+
+/* 1x1 convs with a small output width (N <= 48) whose input is formed on the fly by the op
+ * before them (K % 4 == 0, K <= 240; x, dy, w, BN vectors 16-byte aligned; exact fp32 FMAs):
+ *   pld_pgemm_bn_act: y (=|+=) (act(bn(x)) * gate[img]) . w^T — an EfficientNet block's
+ *       project_conv over bn -> swish -> SE multiply (keras efficientnet block(), used by
+ *       pl_hourglass.py:52-57), replacing pld_bn_apply(gate) + pld_conv2d_fwd; gate [n][K] per
+ *       image of hw rows, or NULL;
+ *   pld_pgemm_bn_bwd: y (=|+=) bnbwd(x, dy) . w^T with bnbwd = pld_bn_bwd's dx for the
+ *       coefficients k12 from pld_bn_bwd_coeffs — the expand_conv's input gradient through the
+ *       expand BN's backward, replacing pld_bn_bwd's apply + pld_conv2d_dgrad.
+ * x, dy [rows][K]; w [N][K] (the native fwd filter, or the dgrad filter [cin][cout]); y [rows][N]. */
+int pld_pgemm_ok(int k, int n);
+int pld_pgemm_bn_act(const float* x, int64_t rows, int k, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, int act, const float* gate, int hw,
+                     const float* w, int n, float* y, int accumulate, void* stream);
+int pld_pgemm_bn_bwd(const float* x, const float* dy, int64_t rows, int k, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, int act,
+                     const float* k12, const float* w, int n, float* y, int accumulate,
+                     void* stream);
+
 /* residual forms (ResNet-50 blocks `Add -> ReLU`, keras resnet block1; ReDWeb
  * BottleneckConvLayer `out += residual; relu` redweb.py:137-165 and FeatureFusionLayer
  * `x_left + x_up` redweb.py:270):  y = act(bn(x) + res);  backward: dz = dy*act'(bn(x)+res),

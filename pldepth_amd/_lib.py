@@ -65,6 +65,10 @@ _SIGS = {
     "pld_bn_apply": (I32, [P, I64, I32, P, P, P, P, I32, P, I32, P, P]),
     "pld_bn_bwd": (I32, [P, P, I64, I32, P, P, P, P, I32, P, P, I32, P, I32, P, P, I32, P, P]),
     "pld_channel_affine_act": (I32, [P, I64, I32, P, P, I32, P, P]),
+    "pld_bn_bwd_coeffs": (I32, [P, P, I64, I32, P, P, P, P, I32, P, P, I32, P, P, P]),
+    "pld_pgemm_ok": (I32, [I32, I32]),
+    "pld_pgemm_bn_act": (I32, [P, I64, I32, P, P, P, P, I32, P, I32, P, I32, P, I32, P]),
+    "pld_pgemm_bn_bwd": (I32, [P, P, I64, I32, P, P, P, P, I32, P, P, I32, P, I32, P]),
     "pld_bn_add_apply": (I32, [P, I64, I32, P, P, P, P, P, I32, P, P]),
     "pld_bn_add_bwd": (I32, [P, P, I64, I32, P, P, P, P, P, I32, P, I32, P, I32, P, P, I32, P,
                              P]),
@@ -114,7 +118,7 @@ _SIGS = {
 }
 
 # functions returning a value rather than a status
-_NON_STATUS = {"pld_last_error", "pld_version", "pld_conv_num_tiles", "pld_conv_num_schedules",
+_NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_tiles", "pld_conv_num_schedules",
                "pld_conv_schedule_class",
                "pld_conv_kernel_kind", "pld_conv_kernel_name",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",

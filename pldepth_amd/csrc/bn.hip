@@ -678,6 +678,38 @@ extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x
                        dgamma, dbeta, param_accumulate, k12, st);
 }
 
+// the reductions + finalize of pld_bn_bwd without its elementwise pass: dgamma/dbeta and the
+// per-channel coefficients k12 = [mean dz | mean dz xhat] for a consumer that applies the
+// backward on the fly (pgemm.hip's PRO_BNBWD)
+extern "C" int pld_bn_bwd_coeffs(const float* x, const float* dy, int64_t rows, int c,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, float* dgamma, float* dbeta,
+                                 int param_accumulate, float* k12, void* ws, void* stream) {
+  PLD_CHECK_ARG(x && dy && mean && invstd && gamma && beta && k12 && ws && rows > 0 && c > 0,
+                "pld_bn_bwd_coeffs: bad args");
+  PLD_CHECK_ARG(rows < (1L << 31), "pld_bn_bwd_coeffs: too many rows");
+  hipStream_t st = as_stream(stream);
+  RedParams p{};
+  p.x = x;
+  p.dy = dy;
+  p.rows = rows;
+  p.C = c;
+  p.mean = mean;
+  p.invstd = invstd;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.act = act;
+  p.dHW = FastDiv(1);
+  p.partial = (double*)ws;
+  int rc = launch_reduce(RED_BNBWD, p, st);
+  if (rc) return rc;
+  int nbx, rpb;
+  red_plan(rows, c, nbx, rpb);
+  bnbwd_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,
+                                                       param_accumulate, k12);
+  return check_launch("bnbwd_finalize_kernel");
+}
+
 extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, const float* mean,
                           const float* invstd, const float* gamma, const float* beta, int act,
                           const float* gate, const float* addn, int hw, float* dx,

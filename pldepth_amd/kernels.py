@@ -458,6 +458,42 @@ def bn_bwd(x, dy, rows, c, mean, invstd, gamma, beta, act, dx, dgamma, dbeta, ga
                      ptr(dgamma), ptr(dbeta), int(param_accumulate), ptr(ws), stream())
 
 
+def bn_bwd_coeffs(x, dy, rows, c, mean, invstd, gamma, beta, act, dgamma, dbeta, k12,
+                  param_accumulate=False):
+    """pld_bn_bwd's reductions + finalize: dgamma, dbeta and k12 [2c] for pgemm_bn_bwd."""
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_bn_bwd_coeffs(ptr(x), ptr(dy), rows, c, ptr(mean), ptr(invstd), ptr(gamma),
+                            ptr(beta), ACT[act], ptr(dgamma), ptr(dbeta), int(param_accumulate),
+                            ptr(k12), ptr(ws), stream())
+
+
+def pgemm_ok(k, n):
+    return bool(lib().pld_pgemm_ok(int(k), int(n)))
+
+
+def pgemm_pays(k, n):
+    """Where the fused pgemm beats the unfused pair (tools/pgemm_micro.py, MI355X, 448^2 batch
+    32): filter K x N <= 4096 floats, i.e. it stays in the scalar cache that feeds the FMAs
+    (1a/2a/2b project, 2a/2b/3a expand dgrad: 26-176 us saved each); at 144 x 40 and 240 x 40
+    the filter streams from L2 per 16-wide chunk and the bf16x3 MFMA pair is faster."""
+    return pgemm_ok(k, n) and k * n <= 4096
+
+
+def pgemm_bn_act(x, rows, k, mean, invstd, gamma, beta, act, w, n, y, gate=None, hw=0,
+                 accumulate=False):
+    """y [rows, n] = (act(bn(x)) * gate[img]) . w^T  (w [n][k])."""
+    lib().pld_pgemm_bn_act(ptr(x), rows, k, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                           ACT[act], ptr(gate), hw, ptr(w), n, ptr(y), int(accumulate), stream())
+
+
+def pgemm_bn_bwd(x, dy, rows, k, mean, invstd, gamma, beta, act, k12, w, n, y,
+                 accumulate=False):
+    """y [rows, n] = bn_bwd(x, dy; k12) . w^T  (w [n][k])."""
+    lib().pld_pgemm_bn_bwd(ptr(x), ptr(dy), rows, k, ptr(mean), ptr(invstd), ptr(gamma),
+                           ptr(beta), ACT[act], ptr(k12), ptr(w), n, ptr(y), int(accumulate),
+                           stream())
+
+
 def bn_add_apply(x, rows, c, mean, invstd, gamma, beta, res, act, y):
     lib().pld_bn_add_apply(ptr(x), rows, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
                            ptr(res), ACT[act], ptr(y), stream())

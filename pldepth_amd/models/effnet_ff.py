@@ -110,6 +110,8 @@ class EffNetFF:
         self.norm_scale = torch.empty(3, device=self.device)
         self.norm_shift = torch.empty(3, device=self.device)
         self.init_weights(seed)
+        # thin-N 1x1 convs with the neighbouring BN (+ act, SE gate) folded in (pgemm.hip)
+        self.fuse_pgemm = True
         self._alloc_activations()
         self.drop_connect = True
         self.seed = seed
@@ -274,6 +276,11 @@ class EffNetFF:
             blk["addn"] = torch.empty(B, cexp, device=dev)
             blk["drop"] = torch.ones(B, device=dev)
             blk["dbn"] = torch.empty(B, oh, ow, cout, device=dev) if blk["residual"] else None
+            # thin-N 1x1 convs with their neighbouring elementwise op folded in (pgemm.hip):
+            # the project conv over BN + swish + SE gate, the expand dgrad over the BN backward
+            blk["fused_project"] = self.fuse_pgemm and K.pgemm_pays(cexp, cout)
+            blk["fused_expand_dgrad"] = (self.fuse_pgemm and blk["ex"] != 1
+                                         and K.pgemm_pays(cexp, blk["cin"]))
             h, w = oh, ow
         new("top_pre", (B, h, w, 1280), grad=False)
         new("top_activation", (B, h, w, 1280))
@@ -285,6 +292,14 @@ class EffNetFF:
         new("pred", (B, H, W, 1))
         # pre-BN gradient scratch, one per distinct shape
         self._gpre = {}
+
+    def _k12_buf(self, c):
+        """BN-backward coefficients [2c] (pgemm_bn_bwd's k12), one scratch per width."""
+        if not hasattr(self, "_k12"):
+            self._k12 = {}
+        if c not in self._k12:
+            self._k12[c] = torch.empty(2 * c, device=self.device)
+        return self._k12[c]
 
     def _gpre_buf(self, shape):
         key = tuple(shape)
@@ -385,20 +400,30 @@ class EffNetFF:
         F = self.frozen
         se_w = (F[blk["se_w1"]].view(blk["cexp"], blk["cse"]), F[blk["se_b1"]],
                 F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]])
-        if training:
-            # the SE squeeze applies BN + swish to dw_pre on the fly and se_excite is written
-            # straight from dw_pre: the block's activation is never materialised
+        if training and blk["fused_project"]:
+            # the SE squeeze applies BN + swish to dw_pre on the fly, and the project conv reads
+            # dw_pre through BN + swish + the SE gate (pgemm): neither the block's activation
+            # nor se_excite is materialised
             K.se_fwd(A[n + "dw_pre"], *se_w, blk["pooled"], blk["z1"], blk["gate"],
                      bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="swish")
-            bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "se_excite"], True, gate=blk["gate"],
-                     hw=oh * ow)
+            K.pgemm_bn_act(A[n + "dw_pre"], rows, blk["cexp"], bn.mean, bn.invstd, bn.gamma,
+                           bn.beta, "swish", blk["project"].w_nat, blk["cout"],
+                           A[n + "project_pre"], gate=blk["gate"], hw=oh * ow)
         else:
-            bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
-            K.se_fwd(A[n + "activation"], *se_w, blk["pooled"], blk["z1"], blk["gate"])
-            self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
-        K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
-                                 math=self._em(oh, ow)),
-                     blk["project"].w_nat, None, A[n + "project_pre"])
+            if training:
+                # the SE squeeze applies BN + swish to dw_pre on the fly and se_excite is written
+                # straight from dw_pre: the block's activation is never materialised
+                K.se_fwd(A[n + "dw_pre"], *se_w, blk["pooled"], blk["z1"], blk["gate"],
+                         bn=(bn.mean, bn.invstd, bn.gamma, bn.beta), act="swish")
+                bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "se_excite"], True,
+                         gate=blk["gate"], hw=oh * ow)
+            else:
+                bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
+                K.se_fwd(A[n + "activation"], *se_w, blk["pooled"], blk["z1"], blk["gate"])
+                self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
+            K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow,
+                                     blk["cout"], math=self._em(oh, ow)),
+                         blk["project"].w_nat, None, A[n + "project_pre"])
         pbn = blk["project_bn"]
         pbn.stats_(A[n + "project_pre"], rows, training)
         out = A[n + "output"]
@@ -538,11 +563,23 @@ class EffNetFF:
             # skip taps already hold the decoder's gradient: accumulate onto it
             is_tap = n + "expand_activation" in SKIP_TAPS
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
-            gpe = self._gpre_buf(A[n + "expand_pre"].shape)
-            blk["expand_bn"].bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
-            K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                       math=self._em(h, w)), gpe,
-                           blk["expand"].w_dg, gx_in)
+            ebn = blk["expand_bn"]
+            if blk["fused_expand_dgrad"]:
+                # the expand BN's reductions, then the expand conv's input gradient reading
+                # (expand_pre, ge) through the BN backward (pgemm): its dx is never materialised
+                k12 = self._k12_buf(blk["cexp"])
+                K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], ebn.mean,
+                                ebn.invstd, ebn.gamma, ebn.beta, "swish", ebn.dgamma, ebn.dbeta,
+                                k12)
+                K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], ebn.mean,
+                               ebn.invstd, ebn.gamma, ebn.beta, "swish", k12,
+                               blk["expand"].w_dg, blk["cin"], gx_in)
+            else:
+                gpe = self._gpre_buf(A[n + "expand_pre"].shape)
+                ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
+                K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
+                                           math=self._em(h, w)), gpe,
+                               blk["expand"].w_dg, gx_in)
         else:
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)
         if blk["residual"]:

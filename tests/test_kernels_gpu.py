@@ -865,3 +865,55 @@ def test_upconv_matches_unfused_path(cuda, n, h, w, c):
     assert rel_err(y, o.detach().permute(0, 2, 3, 1)) < 1e-5
     assert rel_err(dw, w64.grad.permute(2, 3, 1, 0)) < 1e-5
     assert rel_err(dact, a.grad.permute(0, 2, 3, 1)) < 1e-5
+
+
+# --------------------------------------- thin-N 1x1 convs with the neighbouring BN folded in
+@pytest.mark.parametrize("n,hw,k,cout,gate", [(2, 100, 96, 24, True), (3, 57, 144, 40, True),
+                                              (2, 64, 32, 16, False), (1, 300, 240, 40, True),
+                                              (2, 33, 144, 24, False)])
+def test_pgemm_bn_act_and_bn_bwd(cuda, n, hw, k, cout, gate):
+    """pld_pgemm_bn_act == pld_bn_apply(swish, gate) + exact-fp32 1x1 conv, and
+    pld_bn_bwd_coeffs + pld_pgemm_bn_bwd == pld_bn_bwd(swish) + exact-fp32 1x1 dgrad
+    (csrc/pgemm.hip; ragged row counts, every N width class)."""
+    g = torch.Generator(device=cuda).manual_seed(k + cout + hw)
+    rows = n * hw
+    x = torch.randn(n, hw, 1, k, device=cuda, generator=g) * 1.5 + 0.2
+    mean = torch.randn(k, device=cuda, generator=g) * 0.1
+    invstd = torch.rand(k, device=cuda, generator=g) + 0.5
+    gamma = torch.rand(k, device=cuda, generator=g) + 0.5
+    beta = torch.randn(k, device=cuda, generator=g) * 0.1
+    gt = torch.rand(n, k, device=cuda, generator=g) if gate else None
+    wt = torch.randn(1, 1, k, cout, device=cuda, generator=g) / k ** 0.5
+    wn = K.filter_to_native(wt)                      # [cout][k]
+    # forward: reference = apply then conv (fp32 math)
+    a = torch.empty_like(x)
+    K.bn_apply(x, rows, k, mean, invstd, gamma, beta, "swish", a, gate=gt, hw=hw)
+    y_ref = torch.empty(n, hw, 1, cout, device=cuda)
+    K.conv2d_fwd(K.conv_args(a, None, 1, 1, 1, 0, 0, hw, 1, cout, math="fp32"), wn, None, y_ref)
+    y = torch.empty_like(y_ref)
+    K.pgemm_bn_act(x, rows, k, mean, invstd, gamma, beta, "swish", wn, cout, y, gate=gt, hw=hw)
+    # backward: the expand-dgrad form (w = the dgrad filter [cin][cexp] of a cin -> cexp conv)
+    cin = cout
+    w2 = torch.randn(1, 1, cin, k, device=cuda, generator=g) / k ** 0.5
+    wd = K.filter_to_dgrad(w2)                       # [cin][k]
+    dy = torch.randn_like(x)
+    dx_ref = torch.empty_like(x)
+    dg_ref, db_ref = torch.empty(k, device=cuda), torch.empty(k, device=cuda)
+    K.bn_bwd(x, dy, rows, k, mean, invstd, gamma, beta, "swish", dx_ref, dg_ref, db_ref)
+    gx_ref = torch.empty(n, hw, 1, cin, device=cuda)
+    K.conv2d_dgrad(K.conv_args(gx_ref, None, 1, 1, 1, 0, 0, hw, 1, k, math="fp32"), dx_ref, wd,
+                   gx_ref)
+    k12 = torch.empty(2 * k, device=cuda)
+    dg, db = torch.empty(k, device=cuda), torch.empty(k, device=cuda)
+    K.bn_bwd_coeffs(x, dy, rows, k, mean, invstd, gamma, beta, "swish", dg, db, k12)
+    gx = torch.empty_like(gx_ref)
+    K.pgemm_bn_bwd(x, dy, rows, k, mean, invstd, gamma, beta, "swish", k12, wd, cin, gx)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
+    assert rel_err(gx, gx_ref) < 1e-5, rel_err(gx, gx_ref)
+    # accumulate form
+    K.pgemm_bn_act(x, rows, k, mean, invstd, gamma, beta, "swish", wn, cout, y, gate=gt, hw=hw,
+                   accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, 2 * y_ref) < 1e-5
