@@ -61,8 +61,11 @@ def profile_conv(trainer, lr):
     from pldepth_amd._lib import lib
     st = trainer.stream
     recs = []
-    orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad")}
-    mode_of = {"conv2d_fwd": 0, "conv2d_dgrad": 1, "conv2d_wgrad": 2}
+    # conv2d_fwd_bn_stats: the conv + its output's BN statistics (gathered in the thin kernel's
+    # epilogue, else a stats pass): the call's time includes the statistics
+    orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad",
+                                       "conv2d_fwd_bn_stats")}
+    mode_of = {"conv2d_fwd": 0, "conv2d_dgrad": 1, "conv2d_wgrad": 2, "conv2d_fwd_bn_stats": 0}
 
     def flops_of(a):
         # fwd, dX and dW of one conv are the same contraction: 2 * outputs * taps * Cin * Cout

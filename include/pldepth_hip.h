@@ -120,6 +120,18 @@ typedef struct pld_conv_args {
 
 enum { PLD_MATH_FP32 = 0, PLD_MATH_BF16X3 = 1 };
 
+/* conv forward (as pld_conv2d_fwd, no accumulate) followed by the training-mode batch statistics
+ * of its output for the BatchNormalization after it (as pld_bn_stats: eps, momentum, mean,
+ * invstd, optional moving statistics). Where the conv's kernel can gather the per-channel sums
+ * as it stores its tile (thin 1x1 convs: the early EfficientNet expand convs, pl_hourglass.py
+ * via keras efficientnet block()), the output is not read back; otherwise the two calls.
+ * Workspace: pld_conv2d_fwd_bn_stats_workspace_size (besides a->ws for split-K). */
+size_t pld_conv2d_fwd_bn_stats_workspace_size(const pld_conv_args* a);
+int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_ohwi, const float* bias,
+                            float* y, float eps, float momentum, float* mean, float* invstd,
+                            float* moving_mean, float* moving_var, void* ws, size_t ws_bytes,
+                            void* stream);
+
 /* number of implicit-GEMM schedules selectable through pld_conv_args.tile (FP32 math) */
 int pld_conv_num_tiles(void);
 /* the same for a given PLD_MATH_* */

@@ -50,6 +50,9 @@ _SIGS = {
     "pld_conv2d_wgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
     "pld_conv2d_wgrad": (I32, [C.POINTER(ConvArgs), P, P, I32, P, SZ, P]),
     "pld_conv_num_tiles": (I32, []),
+    "pld_conv2d_fwd_bn_stats_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
+    "pld_conv2d_fwd_bn_stats": (I32, [C.POINTER(ConvArgs), P, P, P, F32, F32, P, P, P, P, P, SZ,
+                                      P]),
     "pld_conv_num_schedules": (I32, [I32]),
     "pld_conv_schedule_class": (I32, [I32, I32]),
     "pld_conv_kernel_kind": (I32, [C.POINTER(ConvArgs), I32]),
@@ -122,6 +125,7 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_ti
                "pld_conv_schedule_class",
                "pld_conv_kernel_kind", "pld_conv_kernel_name",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
+               "pld_conv2d_fwd_bn_stats_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",

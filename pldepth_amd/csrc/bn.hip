@@ -512,6 +512,17 @@ extern "C" int pld_bn_stats(const float* x, int64_t rows, int c, float eps, floa
   return check_launch("stats_finalize_kernel");
 }
 
+// internal (conv producers that gather the statistics of their output): finalize only
+extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows, int c,
+                                    float eps, float momentum, float* mean, float* invstd,
+                                    float* moving_mean, float* moving_var, hipStream_t st) {
+  PLD_CHECK_ARG(part && mean && invstd && rows > 0 && c > 0 && nparts > 0,
+                "pld__bn_stats_finish: bad args");
+  stats_finalize_kernel<<<c, 256, 0, st>>>(part, nparts, c, rows, eps, momentum, mean, invstd,
+                                           moving_mean, moving_var);
+  return check_launch("stats_finalize_kernel");
+}
+
 static int bn_apply_impl(const float* x, int64_t rows, int c, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int act,
                          const float* gate, int hw, const float* res, float* y, void* stream) {

@@ -673,7 +673,12 @@ extern "C" int pld__skinny_wgrad(const pld_conv_args* a, const float* dy, float*
 extern "C" int pld__thin_ok(int K, int N);
 extern "C" int pld__thin_geom(const pld_conv_args* a);
 extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias, float* out,
-                              long M, int K, int N, int acc, void* stream);
+                              long M, int K, int N, int acc, void* stream, double* stats);
+extern "C" int pld__thin_stats_parts(long M);
+// bn.hip: BN batch statistics from channel-major fp64 partials (stats_finalize_kernel)
+extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows, int c,
+                                    float eps, float momentum, float* mean, float* invstd,
+                                    float* moving_mean, float* moving_var, hipStream_t st);
 extern "C" int pld__x3_num_cfg(void);
 extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int* occ);
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
@@ -918,7 +923,7 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   if (pld__thin_geom(a) && pld__thin_ok(a->c1, a->cout) && aligned16(a->x1) && aligned16(y) &&
       aligned16(w_ohwi))
     return pld__thin_gemm(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, a->c1, a->cout,
-                          accumulate, stream);
+                          accumulate, stream, nullptr);
   p.bmat = w_ohwi;
   p.bsplit = (const float*)a->w_split;
   p.M = a->n * a->oh * a->ow;
@@ -935,6 +940,46 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   const bool vec16 = vec && (p.c1 % 16 == 0) && (p.c2 % 16 == 0);
   return run_fwd_gemm(p, vec, vec16, a->tile, a->ws, a->ws_bytes, as_stream(stream),
                       "pld_conv2d_fwd", a->math);
+}
+
+// conv forward + the batch statistics of its output for the BatchNormalization that follows:
+// where the kernel the conv runs on can gather them as it stores its tile (thin 1x1), the
+// output is not read back; otherwise pld_conv2d_fwd + pld_bn_stats.
+static bool fwd_stats_fused(const pld_conv_args* a, const float* w_ohwi, const float* y) {
+  return !pld__skinny_eligible(a) && pld__thin_geom(a) && pld__thin_ok(a->c1, a->cout) &&
+         aligned16(a->x1) && aligned16(y) && aligned16(w_ohwi);
+}
+
+extern "C" size_t pld_conv2d_fwd_bn_stats_workspace_size(const pld_conv_args* a) {
+  if (!a || a->n <= 0 || a->oh <= 0 || a->ow <= 0 || a->cout <= 0) return 0;
+  const long rows = (long)a->n * a->oh * a->ow;
+  const size_t fused = sizeof(double) * 2 * (size_t)a->cout * pld__thin_stats_parts(rows);
+  return std::max(fused, pld_channel_reduce_workspace_size(rows, a->cout));
+}
+
+extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_ohwi,
+                                       const float* bias, float* y, float eps, float momentum,
+                                       float* mean, float* invstd, float* moving_mean,
+                                       float* moving_var, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  PLD_CHECK_ARG(a && w_ohwi && y && mean && invstd && ws, "pld_conv2d_fwd_bn_stats: bad args");
+  PLD_CHECK_ARG(ws_bytes >= pld_conv2d_fwd_bn_stats_workspace_size(a),
+                "pld_conv2d_fwd_bn_stats: workspace too small");
+  PLD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr),
+                "pld_conv2d_fwd_bn_stats: moving_mean/moving_var must both be given or both NULL");
+  const long rows = (long)a->n * a->oh * a->ow;
+  if (fwd_stats_fused(a, w_ohwi, y)) {
+    int rc = pld__thin_gemm(a->x1, w_ohwi, bias, y, rows, a->c1, a->cout, 0, stream,
+                            (double*)ws);
+    if (rc) return rc;
+    return pld__bn_stats_finish((const double*)ws, pld__thin_stats_parts(rows), rows, a->cout,
+                                eps, momentum, mean, invstd, moving_mean, moving_var,
+                                as_stream(stream));
+  }
+  int rc = pld_conv2d_fwd(a, w_ohwi, bias, y, 0, stream);
+  if (rc) return rc;
+  return pld_bn_stats(y, rows, a->cout, eps, momentum, mean, invstd, moving_mean, moving_var, ws,
+                      stream);
 }
 
 extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
@@ -1094,7 +1139,7 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   if (pld__thin_geom(a) && pld__thin_ok(a->cout, a->c1) && aligned16(dy) && aligned16(dx1) &&
       aligned16(w_dgrad))
     return pld__thin_gemm(dy, w_dgrad, nullptr, dx1, (long)a->n * a->h * a->w, a->cout, a->c1,
-                          accumulate1, stream);
+                          accumulate1, stream, nullptr);
   // dx[img][iy][ix][ci] = sum_{ty,tx,co} dy[img][iy+ty-pt'][ix+tx-pl'][co] * Wd[ci][ty][tx][co]
   // with pt' = kh-1-pt and the output spatial = the forward input spatial.
   pld_conv_args g = *a;

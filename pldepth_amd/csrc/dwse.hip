@@ -562,18 +562,22 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
     for (int j = 0; j < cse; ++j) acc += dz1[j] * w1[(long)ch * cse + j];
     const float ad = acc / (float)hw;
     addn[(long)img * c + ch] = ad;
-    if (bnpart) {
-      // the block BN's backward partials of this image: sum dz = g A1 + addn A2, sum dz xhat =
-      // g B1 + addn B2 per squeeze split -> [ch][img * rsplit + k][2] (bnbwd_finalize's layout)
-      const double g = gate[(long)img * c + ch];
-      const long plane = (long)gridDim.x * rsplit * c, nparts = (long)gridDim.x * rsplit;
-      for (int k = 0; k < rsplit; ++k) {
-        const long o = ((long)img * rsplit + k) * c + ch;
-        const double d0 = g * part4[o] + (double)ad * part4[plane + o];
-        const double d1 = g * part4[2 * plane + o] + (double)ad * part4[3 * plane + o];
-        *reinterpret_cast<double2*>(bnpart + ((long)ch * nparts + (long)img * rsplit + k) * 2) =
-            make_double2(d0, d1);
-      }
+    if (bnpart) dz2[ch] = ad;  // dz2 is no longer read: the slice's addn for the BN partials
+  }
+  if (bnpart) {
+    // the block BN's backward partials of this image: sum dz = g A1 + addn A2, sum dz xhat =
+    // g B1 + addn B2 per squeeze split -> [ch][img * rsplit + k][2] (bnbwd_finalize's layout);
+    // every (channel, split) pair of the slice on its own thread
+    __syncthreads();
+    const long plane = (long)gridDim.x * rsplit * c, nparts = (long)gridDim.x * rsplit;
+    for (int e = threadIdx.x; e < (ce - cb) * rsplit; e += SE_THREADS) {
+      const int ch = cb + e / rsplit, k = e % rsplit;
+      const double g = gate[(long)img * c + ch], ad = dz2[ch];
+      const long o = ((long)img * rsplit + k) * c + ch;
+      const double d0 = g * part4[o] + ad * part4[plane + o];
+      const double d1 = g * part4[2 * plane + o] + ad * part4[3 * plane + o];
+      *reinterpret_cast<double2*>(bnpart + ((long)ch * nparts + (long)img * rsplit + k) * 2) =
+          make_double2(d0, d1);
     }
   }
 }

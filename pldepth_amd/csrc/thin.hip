@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
                                                       const float* __restrict__ b,
                                                       const float* __restrict__ bias,
                                                       float* __restrict__ out, int M, int N,
-                                                      int acc) {
+                                                      int acc, double* __restrict__ stats) {
   constexpr int LA = KR + THIN_PAD;  // LDS row stride of the staged a tile
   constexpr int LO = CH + THIN_PAD;  // LDS row stride of a wave's output chunk
   __shared__ __attribute__((aligned(16))) float sa[64 * LA];
@@ -68,6 +68,28 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
     for (int j = 0; j < CH; j += 4)
       *reinterpret_cast<float4*>(sw + lane * LO + j) = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
     __builtin_amdgcn_wave_barrier();
+    if (stats) {
+      // BN batch statistics of the output (the BatchNormalization that follows the conv):
+      // per column, sum and sum of squares over this workgroup's rows in fp64 — lane (j, part)
+      // sums rows part, part + 64/CH, ... of column j, then a fixed butterfly over the parts.
+      // Partials [N][gridDim.x][2] (bn.hip's finalize layout).
+      constexpr int NP = 64 / CH;
+      const int j = lane % CH, part = lane / CH;
+      double s1 = 0.0, s2 = 0.0;
+      for (int r = part; r < rows; r += NP) {
+        const double v = (double)sw[r * LO + j];
+        s1 += v;
+        s2 += v * v;
+      }
+#pragma unroll
+      for (int o = CH; o < 64; o <<= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if (lane < CH)
+        *reinterpret_cast<double2*>(stats + ((long)(n0 + j) * gridDim.x + blockIdx.x) * 2) =
+            make_double2(s1, s2);
+    }
     // rows x CH chunk: CH/4 lanes per row, 64 / (CH/4) rows per store instruction
     constexpr int QPR = CH / 4;
 #pragma unroll
@@ -87,12 +109,13 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
 
 template <int KR>
 static void thin_launch(const float* a, const float* b, const float* bias, float* out, int M,
-                        int N, int acc, hipStream_t st) {
+                        int N, int acc, double* stats, hipStream_t st) {
   const unsigned grid = (unsigned)cdiv(M, 64);
   // CH = 16 only when the chunks split evenly over the 4 waves (N = 144: 18 chunks of 8 balance
   // 5/5/4/4, 9 chunks of 16 would leave three waves idle a third of the time)
-  if (N % 64 == 0 && N >= 128) thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
-  else thin1x1_kernel<KR, 8><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc);
+  if (N % 64 == 0 && N >= 128)
+    thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc, stats);
+  else thin1x1_kernel<KR, 8><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc, stats);
 }
 
 static bool thin_kr_ok(int kr) { return kr % 8 == 0 && kr >= 8 && kr <= 48; }
@@ -120,8 +143,11 @@ extern "C" int pld__thin_geom(const pld_conv_args* a) {
          a->oh == a->h && a->ow == a->w;
 }
 
+// stats: NULL, or [N][cdiv(M, 64)][2] fp64 BN partials of the output (pld__thin_stats_parts)
+extern "C" int pld__thin_stats_parts(long M) { return (int)cdiv(M, 64); }
+
 extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias, float* out,
-                              long M, int K, int N, int acc, void* stream) {
+                              long M, int K, int N, int acc, void* stream, double* stats) {
   PLD_CHECK_ARG(a && b && out && M > 0 && aligned16(a) && aligned16(out) && aligned16(b),
                 "thin1x1: bad args");
   PLD_CHECK_ARG(M * (long)(K > N ? K : N) < (1L << 31), "thin1x1: tensor too large");
@@ -129,12 +155,12 @@ extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias,
   hipStream_t st = as_stream(stream);
   const int m = (int)M;
   switch (K) {
-    case 8: thin_launch<8>(a, b, bias, out, m, N, acc, st); break;
-    case 16: thin_launch<16>(a, b, bias, out, m, N, acc, st); break;
-    case 24: thin_launch<24>(a, b, bias, out, m, N, acc, st); break;
-    case 32: thin_launch<32>(a, b, bias, out, m, N, acc, st); break;
-    case 40: thin_launch<40>(a, b, bias, out, m, N, acc, st); break;
-    default: thin_launch<48>(a, b, bias, out, m, N, acc, st); break;
+    case 8: thin_launch<8>(a, b, bias, out, m, N, acc, stats, st); break;
+    case 16: thin_launch<16>(a, b, bias, out, m, N, acc, stats, st); break;
+    case 24: thin_launch<24>(a, b, bias, out, m, N, acc, stats, st); break;
+    case 32: thin_launch<32>(a, b, bias, out, m, N, acc, stats, st); break;
+    case 40: thin_launch<40>(a, b, bias, out, m, N, acc, stats, st); break;
+    default: thin_launch<48>(a, b, bias, out, m, N, acc, stats, st); break;
   }
   return check_launch("thin1x1_kernel");
 }

@@ -370,9 +370,9 @@ def _end(args, tile_in):
     args.tile = tile_in
 
 
-def conv2d_fwd(args, w_native, bias, y, accumulate=False):
-    tile_in = _begin(args)
-    _set_split(args, w_native)
+def _fwd_schedule(args, w_native, bias, y):
+    """Resolve args.tile for a forward conv (autotuned per shape when -1) and size its split-K
+    workspace."""
     if args.tile < 0:
         scratch = None
 
@@ -385,8 +385,30 @@ def conv2d_fwd(args, w_native, bias, y, accumulate=False):
                                  stream())
         args.tile = _tune("fwd", args, run)
     _splitk_ws(args, lib().pld_conv2d_fwd_workspace_size)
+
+
+def conv2d_fwd(args, w_native, bias, y, accumulate=False):
+    tile_in = _begin(args)
+    _set_split(args, w_native)
+    _fwd_schedule(args, w_native, bias, y)
     lib().pld_conv2d_fwd(C.byref(args), ptr(w_native), ptr(bias), ptr(y), int(accumulate),
                          stream())
+    _end(args, tile_in)
+    return y
+
+
+def conv2d_fwd_bn_stats(args, w_native, bias, y, mean, invstd, moving_mean=None,
+                        moving_var=None, eps=1e-3, momentum=0.99):
+    """conv2d_fwd + bn_stats of its output (pld_conv2d_fwd_bn_stats: the statistics gathered by
+    the conv kernel's epilogue where it supports it)."""
+    tile_in = _begin(args)
+    _set_split(args, w_native)
+    _fwd_schedule(args, w_native, bias, y)
+    need = lib().pld_conv2d_fwd_bn_stats_workspace_size(C.byref(args))
+    ws = workspace(need, "bnstats")
+    lib().pld_conv2d_fwd_bn_stats(C.byref(args), ptr(w_native), ptr(bias), ptr(y), eps,
+                                  momentum, ptr(mean), ptr(invstd), ptr(moving_mean),
+                                  ptr(moving_var), ptr(ws), need, stream())
     _end(args, tile_in)
     return y
 

@@ -293,6 +293,15 @@ class EffNetFF:
         # pre-BN gradient scratch, one per distinct shape
         self._gpre = {}
 
+    def tap(self, name):
+        """An activation by its Keras layer name, materialised on demand where the training
+        forward folds it into its consumer (stem_activation: block1a's depthwise prologue)."""
+        if name == "stem_activation":
+            B, h, w = self.B, self.H // 2, self.W // 2
+            self.stem_bn.apply(self.act["stem_pre"], B * h * w, "swish",
+                               self.act["stem_activation"], True)
+        return self.act[name]
+
     def _k12_buf(self, c):
         """BN-backward coefficients [2c] (pgemm_bn_bwd's k12), one scratch per width."""
         if not hasattr(self, "_k12"):
@@ -326,11 +335,15 @@ class EffNetFF:
         h, w = self.H // 2, self.W // 2
         args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none",
                  math=self._em(h, w))
-        K.conv2d_fwd(args, self.stem.w_nat, None, A["stem_pre"])
         rows = B * h * w
-        self.stem_bn.stats_(A["stem_pre"], rows, training)
-        self.stem_bn.apply(A["stem_pre"], rows, "swish", A["stem_activation"], training)
-        x = A["stem_activation"]
+        self._conv_bn(args, self.stem.w_nat, None, A["stem_pre"], self.stem_bn, rows, training)
+        if training:
+            # stem BN + swish applied by block1a's depthwise conv as it reads its taps: the stem
+            # activation (its only consumer in training) is never materialised
+            x = None
+        else:
+            self.stem_bn.apply(A["stem_pre"], rows, "swish", A["stem_activation"], training)
+            x = A["stem_activation"]
         for li, blk in enumerate(self.blocks):
             x = self._block_fwd(blk, x, training, step, li)
         h, w = x.shape[1], x.shape[2]
@@ -376,11 +389,11 @@ class EffNetFF:
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
         pt, pl = blk["pad"]
         if blk["ex"] != 1:
-            K.conv2d_fwd(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                     math=self._em(h, w)),
-                         blk["expand"].w_nat, None, A[n + "expand_pre"])
             ebn = blk["expand_bn"]
-            ebn.stats_(A[n + "expand_pre"], B * h * w, training)
+            self._conv_bn(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
+                                      math=self._em(h, w)),
+                          blk["expand"].w_nat, None, A[n + "expand_pre"], ebn, B * h * w,
+                          training)
             if training and n + "expand_activation" not in SKIP_TAPS:
                 # BN + swish fused into the depthwise conv's input read: the activation is
                 # never materialised (only the decoder's skip taps need it)
@@ -392,6 +405,11 @@ class EffNetFF:
                           training)
                 K.dwconv_fwd(A[n + "expand_activation"], self.frozen[blk["dw"]], blk["k"],
                              blk["s"], pt, pl, A[n + "dw_pre"])
+        elif x is None:  # block1a in training: the stem's pre-BN output through BN + swish
+            sbn = self.stem_bn
+            K.dwconv_fwd(A["stem_pre"], self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl,
+                         A[n + "dw_pre"], bn=(sbn.mean, sbn.invstd, sbn.gamma, sbn.beta),
+                         act="swish")
         else:
             K.dwconv_fwd(x, self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl, A[n + "dw_pre"])
         rows = B * oh * ow
@@ -436,6 +454,16 @@ class EffNetFF:
                 drop = blk["drop"]
             K.residual_add(out, drop, x, out)
         return out
+
+    def _conv_bn(self, args, w_nat, bias, out, bn, rows, training):
+        """conv forward + the batch statistics of its output for the BN after it (training: in
+        the conv's epilogue where its kernel supports it; inference: the moving statistics)."""
+        if training:
+            K.conv2d_fwd_bn_stats(args, w_nat, bias, out, bn.mean, bn.invstd, bn.mmean, bn.mvar,
+                                  bn.eps, bn.momentum)
+        else:
+            K.conv2d_fwd(args, w_nat, bias, out)
+            bn.stats_(out, rows, training)
 
     def _gate_mul(self, a, gate, y):
         """inference path: y = a * gate[img][c] (a BN apply with identity statistics is exact:

@@ -376,7 +376,7 @@ def test_forward_batch32_bench_policy(cuda, model):
         O, kw = OE, {}
         names = ["stem_activation", "block2a_output", "block3a_expand_activation",
                  "block5c_output", "block7a_output", "top_activation"]
-        mine = lambda n: eng.act[n]
+        mine = eng.tap
     else:
         from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input
         eng = RedWebFF((H, H, 3), B, seed=0, conv_math="auto")

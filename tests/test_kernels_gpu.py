@@ -917,3 +917,29 @@ def test_pgemm_bn_act_and_bn_bwd(cuda, n, hw, k, cout, gate):
                    accumulate=True)
     torch.cuda.synchronize()
     assert rel_err(y, 2 * y_ref) < 1e-5
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 20, 17, 16, 96), (3, 8, 8, 24, 144),
+                                            (2, 9, 7, 40, 240), (1, 5, 6, 48, 64)])
+def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
+    """pld_conv2d_fwd_bn_stats (BN statistics gathered in the thin 1x1 kernel's epilogue, or
+    conv + pld_bn_stats where the kernel cannot) == pld_conv2d_fwd + pld_bn_stats."""
+    g = torch.Generator(device=cuda).manual_seed(cin * cout + h)
+    x = torch.randn(n, h, w, cin, device=cuda, generator=g)
+    wt = torch.randn(1, 1, cin, cout, device=cuda, generator=g) / cin ** 0.5
+    wn = K.filter_to_native(wt)
+    rows = n * h * w
+    args = K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, cout, math="fp32")
+    y_ref = torch.empty(n, h, w, cout, device=cuda)
+    K.conv2d_fwd(args, wn, None, y_ref)
+    m_ref, i_ref = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+    mm_ref, mv_ref = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+    K.bn_stats(y_ref, rows, cout, m_ref, i_ref, mm_ref, mv_ref)
+    y = torch.empty_like(y_ref)
+    m, i = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+    mm, mv = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+    K.conv2d_fwd_bn_stats(args, wn, None, y, m, i, mm, mv)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    for a, b in ((m, m_ref), (i, i_ref), (mm, mm_ref), (mv, mv_ref)):
+        assert rel_err(a, b) < 1e-6, rel_err(a, b)

@@ -66,7 +66,7 @@ def test_forward_activations(step_results):
     # block output checks it; block3a's is a decoder skip tap and stays materialised
     for name in ["stem_activation", "block2a_output", "block3a_expand_activation",
                  "block5c_output", "top_activation"]:
-        e = rel(eng.act[name], taps[name].permute(0, 2, 3, 1))
+        e = rel(eng.tap(name), taps[name].permute(0, 2, 3, 1))
         assert e < TOL, (name, e)
     assert rel(r["pred"], r["pred_ref"]) < TOL
 
@@ -166,6 +166,6 @@ def test_forward_448_conv_policy(cuda, policy):
         pred_ref = OE.forward(P, torch.tensor(x, dtype=torch.float64), taps=taps)
     for name in ["stem_activation", "block2a_output", "block3a_expand_activation",
                  "block4a_output", "block5c_output", "block7a_output", "top_activation"]:
-        e = rel(eng.act[name], taps[name].permute(0, 2, 3, 1))
+        e = rel(eng.tap(name), taps[name].permute(0, 2, 3, 1))
         assert e < TOL, (name, e)
     assert rel(pred, pred_ref) < TOL
