@@ -350,6 +350,17 @@ int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, const float* w
                       int pad_t, int pad_l, int oh, int ow, const float* mean,
                       const float* invstd, const float* gamma, const float* beta, int act,
                       float* y, void* stream);
+/* pld_dwconv_fwd_bn + the training-mode batch statistics of its output y for the block's
+ * BatchNormalization after the depthwise conv (eps, momentum, y_mean, y_invstd, optional moving
+ * statistics: as pld_bn_stats), gathered in the conv's epilogue where the tiled kernel runs
+ * (c % 16 == 0), else a pld_bn_stats pass. Workspace: pld_dwconv_fwd_bn_stats_workspace_size. */
+size_t pld_dwconv_fwd_bn_stats_workspace_size(int n, int oh, int ow, int c, int s);
+int pld_dwconv_fwd_bn_stats(const float* x, int n, int h, int w, int c, const float* wdw, int k,
+                            int s, int pad_t, int pad_l, int oh, int ow, const float* mean,
+                            const float* invstd, const float* gamma, const float* beta, int act,
+                            float* y, float eps, float momentum, float* y_mean, float* y_invstd,
+                            float* y_moving_mean, float* y_moving_var, void* ws, size_t ws_bytes,
+                            void* stream);
 int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw, int k, int s,
                      int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
                      void* stream);

@@ -95,6 +95,9 @@ _SIGS = {
     "pld_dwconv_fwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
     "pld_dwconv_fwd_bn": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P, P,
                                 P, I32, P, P]),
+    "pld_dwconv_fwd_bn_stats_workspace_size": (SZ, [I32, I32, I32, I32, I32]),
+    "pld_dwconv_fwd_bn_stats": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P,
+                                      P, P, P, I32, P, F32, F32, P, P, P, P, P, SZ, P]),
     "pld_dwconv_dgrad": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, I32, P]),
     "pld_se_workspace_size": (SZ, [I32, I32, I32, I32]),
     "pld_se_fwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
@@ -126,6 +129,7 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_ti
                "pld_conv_kernel_kind", "pld_conv_kernel_name",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_conv2d_fwd_bn_stats_workspace_size",
+               "pld_dwconv_fwd_bn_stats_workspace_size",
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",

@@ -602,6 +602,19 @@ static DwGeom dw_geom(int n, int h, int w, int c, int s, int pt, int pl, int oh,
   return g;
 }
 
+// dwtile.hip: the LDS-tiled forward (C % 16 == 0), optionally gathering the output's BN partials
+extern "C" int pld__dw_tiled_ok(int k, int s, int c);
+extern "C" int pld__dw_tiled_parts(int n, int oh, int ow, int s, int c);
+extern "C" int pld__dw_fwd_tiled(const float* x, int n, int h, int w, int c, const float* wdw,
+                                 int k, int s, int pad_t, int pad_l, int oh, int ow,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, float* y, double* stats,
+                                 hipStream_t st);
+// bn.hip
+extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows, int c,
+                                    float eps, float momentum, float* mean, float* invstd,
+                                    float* moving_mean, float* moving_var, hipStream_t st);
+
 template <int K, int S, int T, int R>
 static void dw_fwd_launch(const float* x, const float* wdw, DwGeom& g, float* y, hipStream_t st) {
   const int rgroups = (g.oh + R - 1) / R;
@@ -627,9 +640,12 @@ extern "C" int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, con
   PLD_CHECK_ARG((long)n * h * w * c < (1L << 31) && (long)n * oh * ow * c < (1L << 31),
                 "pld_dwconv_fwd: tensor too large for 32-bit indexing");
   PLD_CHECK_ARG(s == 1 || s == 2, "pld_dwconv_fwd: stride %d unsupported (1, 2)", s);
+  hipStream_t st = as_stream(stream);
+  if (pld__dw_tiled_ok(k, s, c) && aligned16(x) && aligned16(y) && aligned16(wdw))
+    return pld__dw_fwd_tiled(x, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, mean, invstd, gamma,
+                             beta, act, y, nullptr, st);
   DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
   g.mean = mean; g.invstd = invstd; g.gamma = gamma; g.beta = beta; g.act = act;
-  hipStream_t st = as_stream(stream);
   if (k == 3 && s == 1) dw_fwd_launch<3, 1, 4, 4>(x, wdw, g, y, st);
   else if (k == 3) dw_fwd_launch<3, 2, 2, 4>(x, wdw, g, y, st);
   else if (k == 5 && s == 1) dw_fwd_launch<5, 1, 4, 4>(x, wdw, g, y, st);
@@ -639,6 +655,45 @@ extern "C" int pld_dwconv_fwd_bn(const float* x, int n, int h, int w, int c, con
     return PLD_ERR_UNSUPPORTED;
   }
   return check_launch("dwconv_fwd_kernel");
+}
+
+extern "C" size_t pld_dwconv_fwd_bn_stats_workspace_size(int n, int oh, int ow, int c, int s) {
+  if (n <= 0 || oh <= 0 || ow <= 0 || c <= 0) return 0;
+  const size_t fused = sizeof(double) * 2 * (size_t)c * pld__dw_tiled_parts(n, oh, ow, s, c);
+  return std::max(fused, pld_channel_reduce_workspace_size((int64_t)n * oh * ow, c));
+}
+
+extern "C" int pld_dwconv_fwd_bn_stats(const float* x, int n, int h, int w, int c,
+                                       const float* wdw, int k, int s, int pad_t, int pad_l,
+                                       int oh, int ow, const float* mean, const float* invstd,
+                                       const float* gamma, const float* beta, int act, float* y,
+                                       float eps, float momentum, float* y_mean, float* y_invstd,
+                                       float* y_moving_mean, float* y_moving_var, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  PLD_CHECK_ARG(y_mean && y_invstd && ws &&
+                    ws_bytes >= pld_dwconv_fwd_bn_stats_workspace_size(n, oh, ow, c, s),
+                "pld_dwconv_fwd_bn_stats: bad statistics arguments / workspace too small");
+  PLD_CHECK_ARG((y_moving_mean == nullptr) == (y_moving_var == nullptr),
+                "pld_dwconv_fwd_bn_stats: moving statistics must both be given or both NULL");
+  PLD_CHECK_ARG(x && wdw && y && n > 0 && h > 0 && w > 0 && c > 0 && oh > 0 && ow > 0,
+                "pld_dwconv_fwd_bn_stats: bad args");
+  PLD_CHECK_ARG((long)n * h * w * c < (1L << 31) && (long)n * oh * ow * c < (1L << 31),
+                "pld_dwconv_fwd_bn_stats: tensor too large for 32-bit indexing");
+  PLD_CHECK_ARG(!mean || (invstd && gamma && beta), "pld_dwconv_fwd_bn_stats: incomplete BN");
+  hipStream_t st = as_stream(stream);
+  const int64_t rows = (int64_t)n * oh * ow;
+  if (pld__dw_tiled_ok(k, s, c) && aligned16(x) && aligned16(y) && aligned16(wdw)) {
+    int rc = pld__dw_fwd_tiled(x, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, mean, invstd,
+                               gamma, beta, act, y, (double*)ws, st);
+    if (rc) return rc;
+    return pld__bn_stats_finish((const double*)ws, pld__dw_tiled_parts(n, oh, ow, s, c), rows, c,
+                                eps, momentum, y_mean, y_invstd, y_moving_mean, y_moving_var, st);
+  }
+  int rc = pld_dwconv_fwd_bn(x, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, mean, invstd, gamma,
+                             beta, act, y, stream);
+  if (rc) return rc;
+  return pld_bn_stats(y, rows, c, eps, momentum, y_mean, y_invstd, y_moving_mean, y_moving_var,
+                      ws, stream);
 }
 
 extern "C" int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const float* wdw, int k,

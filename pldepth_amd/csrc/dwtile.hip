@@ -1,0 +1,263 @@
+// DepthwiseConv2D forward, LDS-tiled (keras efficientnet block(): DepthwiseConv2D k3/k5,
+// stride 1 'same' or stride 2 after ZeroPadding2D; frozen filters, pl_hourglass.py:52-57), with
+// the block's expand BN + swish applied to the input as it is staged and, optionally, the batch
+// statistics of the output (the BN that follows) gathered in the epilogue.
+//
+// A workgroup owns a TO-wide output tile of 4 CQ = 32 channels (the last group masked when
+// C % 32 == 16). The
+// ((TO - 1) S + K)^2 input window of those channels is read once (coalesced: CQ * 16 contiguous
+// bytes per pixel), activated once per element (the register-window kernel in dwse.hip
+// re-activated every overlapping window load: ~4x the exp / rcp work at k5) and stored in LDS,
+// for stride 2 with even and odd columns in separate planes so that neighbouring output columns
+// read neighbouring LDS addresses. Each thread then owns one channel quad, one output column
+// and R rows: it walks the (R - 1) S + K input rows of its column window once, feeding every tap
+// of every output row it reaches from registers (filter taps preloaded), in the same (ty, tx)
+// summation order as the direct loop. Statistics: per-thread fp64 sums of its outputs, combined
+// over the workgroup in a fixed order into [C][tiles][2] partials (bn.hip's finalize layout).
+#include <algorithm>
+
+#include "common.h"
+
+namespace pld {
+namespace dwt {
+
+struct Geo {
+  const float* x;
+  const float* w;       // [K][K][C]
+  float* y;
+  const float* mean;    // input prologue act(bn(x)) or NULL
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  double* stats;        // [C][gridDim.x][2] or NULL
+  int n, h, wd, c, oh, ow, pt, pl;
+  int tiles_x, tiles_y;
+};
+
+__device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
+  acc.x += v.x * f.x;
+  acc.y += v.y * f.y;
+  acc.z += v.z * f.z;
+  acc.w += v.w * f.w;
+  return acc;
+}
+
+// output rows per tile: 4 per thread (the k5 filter, 25 float4 taps, stays in registers)
+__host__ __device__ constexpr int tile_rows(int s, int cq) { return (256 / (cq * (s == 1 ? 16 : 8))) * (s == 1 ? 4 : 2); }
+
+template <int K, int S, int CQ, int ACT>  // ACT < 0: no prologue
+__global__ __launch_bounds__(256) void dw_fwd_tile_kernel(Geo g) {
+  constexpr int TO = S == 1 ? 16 : 8;             // output tile width
+  constexpr int TOH = tile_rows(S, CQ);           // output tile height
+  constexpr int TI = (TO - 1) * S + K;            // input window width
+  constexpr int TIR = (TOH - 1) * S + K;          // input window height
+  constexpr int TIH = (TI + 1) / 2;               // stride 2: columns per parity plane
+  constexpr int COLS = S == 1 ? TI : 2 * TIH;     // LDS columns (parity planes side by side)
+  constexpr int RGN = 256 / (CQ * TO);            // row groups
+  constexpr int R = TOH / RGN;                    // output rows per thread
+  constexpr int NR = (R - 1) * S + K;             // input rows a thread walks
+  constexpr int NE = TIR * TI * CQ;               // window float4s
+  constexpr int NL = (NE + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float4 tile[];  // [TI][COLS][CQ]
+  const int tid = threadIdx.x;
+  const int sp = blockIdx.x;
+  const int img = sp / (g.tiles_x * g.tiles_y);
+  const int rr = sp - img * g.tiles_x * g.tiles_y;
+  const int oy0 = (rr / g.tiles_x) * TOH, ox0 = (rr % g.tiles_x) * TO;
+  const int cb = blockIdx.y * CQ * 4;             // first channel of the group
+  const int iy0 = oy0 * S - g.pt, ix0 = ox0 * S - g.pl;
+  const float* xb = g.x + (long)img * g.h * g.wd * g.c + cb;
+
+  // ---- stage the window: loads first, then the prologue and the LDS stores ----
+  float4 v[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = tid + 256 * i;
+    const int q = e % CQ, px = e / CQ;
+    const int wy = px / TI, wx = px - wy * TI;
+    const int iy = iy0 + wy, ix = ix0 + wx;
+    const bool ok = e < NE && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd &&
+                    cb + 4 * q < g.c;
+    v[i] = ok ? *reinterpret_cast<const float4*>(xb + ((long)iy * g.wd + ix) * g.c + 4 * q)
+              : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = tid + 256 * i;
+    if (e >= NE) break;
+    const int q = e % CQ, px = e / CQ;
+    const int wy = px / TI, wx = px - wy * TI;
+    const int iy = iy0 + wy, ix = ix0 + wx;
+    float4 a = v[i];
+    if (ACT >= 0 && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd &&
+        cb + 4 * q < g.c) {
+      // bn_apply's arithmetic, then the activation (TF pads the activated map with zeros)
+      const int c0 = cb + 4 * q;
+      const float4 mu = *reinterpret_cast<const float4*>(g.mean + c0);
+      const float4 is = *reinterpret_cast<const float4*>(g.invstd + c0);
+      const float4 ga = *reinterpret_cast<const float4*>(g.gamma + c0);
+      const float4 be = *reinterpret_cast<const float4*>(g.beta + c0);
+      a = make_float4(act_fwd(ACT, ((a.x - mu.x) * is.x) * ga.x + be.x),
+                      act_fwd(ACT, ((a.y - mu.y) * is.y) * ga.y + be.y),
+                      act_fwd(ACT, ((a.z - mu.z) * is.z) * ga.z + be.z),
+                      act_fwd(ACT, ((a.w - mu.w) * is.w) * ga.w + be.w));
+    }
+    const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
+    tile[(wy * COLS + col) * CQ + q] = a;
+  }
+  const int q = tid % CQ, oc = (tid / CQ) % TO, rg = tid / (CQ * TO);
+  const bool qok = cb + 4 * q < g.c;  // the last group of a C % 32 == 16 layer is half full
+  const float* fq = g.w + (qok ? cb + 4 * q : 0);  // this thread's filter quad: tap t at fq + t C
+  float4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto lds_row = [&](int wy, float4 (&row)[K]) {
+#pragma unroll
+    for (int tx = 0; tx < K; ++tx) {
+      const int wx = oc * S + tx;
+      const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
+      row[tx] = tile[(wy * COLS + col) * CQ + q];
+    }
+  };
+  if constexpr (K == 3) {
+    // the 9 taps in registers; each of the (R - 1) S + K input rows of the column window read
+    // once and fed to every output row it reaches
+    float4 f[K][K];
+#pragma unroll
+    for (int ty = 0; ty < K; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < K; ++tx) f[ty][tx] = *reinterpret_cast<const float4*>(fq + (ty * K + tx) * g.c);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      float4 row[K];
+      lds_row(rg * R * S + j, row);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int ty = j - r * S;  // compile-time after unrolling
+        if (ty < 0 || ty >= K) continue;
+#pragma unroll
+        for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[ty][tx]);
+      }
+    }
+  } else {
+    // k5: one filter row (5 taps) in registers at a time, ty outer; each output row re-reads
+    // its input row per ty (25 taps in registers plus the unrolled window do not fit)
+    __syncthreads();
+#pragma unroll 1
+    for (int ty = 0; ty < K; ++ty) {
+      float4 f[K];
+#pragma unroll
+      for (int tx = 0; tx < K; ++tx) f[tx] = *reinterpret_cast<const float4*>(fq + (ty * K + tx) * g.c);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float4 row[K];
+        lds_row(rg * R * S + r * S + ty, row);
+#pragma unroll
+        for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[tx]);
+      }
+    }
+  }
+  // ---- store (+ statistics) ----
+  const int ox = ox0 + oc;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ox < g.ow && qok) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int oy = oy0 + rg * R + r;
+      if (oy >= g.oh) break;
+      *reinterpret_cast<float4*>(g.y + (((long)img * g.oh + oy) * g.ow + ox) * g.c + cb + 4 * q) =
+          acc[r];
+      if (g.stats) {
+        const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double d = a4[u];
+          s1[u] += d;
+          s2[u] += d * d;
+        }
+      }
+    }
+  }
+  if (!g.stats) return;
+  __syncthreads();  // the window is no longer read: reuse it for the fixed-order combine
+  double* red = reinterpret_cast<double*>(tile);  // [256][8]
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    red[tid * 8 + u] = s1[u];
+    red[tid * 8 + 4 + u] = s2[u];
+  }
+  __syncthreads();
+  if (tid < CQ && qok) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = red[tid * 8 + u];
+    for (int j = 1; j < 256 / CQ; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] += red[(tid + CQ * j) * 8 + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<double2*>(g.stats + ((long)(cb + 4 * tid + u) * gridDim.x + sp) * 2) =
+          make_double2(t[u], t[4 + u]);
+  }
+}
+
+template <int K, int S, int CQ>
+static size_t lds_bytes() {
+  constexpr int TO = S == 1 ? 16 : 8;
+  constexpr int TI = (TO - 1) * S + K;
+  constexpr int TIR = (tile_rows(S, CQ) - 1) * S + K;
+  constexpr int COLS = S == 1 ? TI : 2 * ((TI + 1) / 2);
+  const size_t win = sizeof(float4) * TIR * COLS * CQ;
+  return std::max(win, sizeof(double) * 256 * 8);
+}
+
+template <int K, int S, int CQ>
+static void launch(Geo& g, int act, hipStream_t st) {
+  constexpr int TO = S == 1 ? 16 : 8;
+  g.tiles_x = (int)cdiv(g.ow, TO);
+  g.tiles_y = (int)cdiv(g.oh, tile_rows(S, CQ));
+  dim3 grid(g.tiles_x * g.tiles_y * g.n, (int)cdiv(g.c, 4 * CQ));
+  const size_t lds = lds_bytes<K, S, CQ>();
+  if (!g.mean) dw_fwd_tile_kernel<K, S, CQ, -1><<<grid, 256, lds, st>>>(g);
+  else if (act == ACT_SWISH) dw_fwd_tile_kernel<K, S, CQ, ACT_SWISH><<<grid, 256, lds, st>>>(g);
+  else if (act == ACT_RELU) dw_fwd_tile_kernel<K, S, CQ, ACT_RELU><<<grid, 256, lds, st>>>(g);
+  else if (act == ACT_SIGMOID) dw_fwd_tile_kernel<K, S, CQ, ACT_SIGMOID><<<grid, 256, lds, st>>>(g);
+  else dw_fwd_tile_kernel<K, S, CQ, ACT_NONE><<<grid, 256, lds, st>>>(g);
+}
+
+}  // namespace dwt
+}  // namespace pld
+
+using namespace pld;
+
+// eligible: k 3 / 5, stride 1 / 2, C % 16 == 0, 16-byte aligned tensors
+extern "C" int pld__dw_tiled_ok(int k, int s, int c) {
+  return (k == 3 || k == 5) && (s == 1 || s == 2) && c % 16 == 0;
+}
+
+extern "C" int pld__dw_tiled_parts(int n, int oh, int ow, int s, int c) {
+  const int to = s == 1 ? 16 : 8, toh = dwt::tile_rows(s, 8);
+  return (int)(cdiv(oh, toh) * cdiv(ow, to) * n);
+}
+
+extern "C" int pld__dw_fwd_tiled(const float* x, int n, int h, int w, int c, const float* wdw,
+                                 int k, int s, int pad_t, int pad_l, int oh, int ow,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, float* y, double* stats,
+                                 hipStream_t st) {
+  dwt::Geo g{};
+  g.x = x; g.w = wdw; g.y = y;
+  g.mean = mean; g.invstd = invstd; g.gamma = gamma; g.beta = beta;
+  g.stats = stats;
+  g.n = n; g.h = h; g.wd = w; g.c = c; g.oh = oh; g.ow = ow; g.pt = pad_t; g.pl = pad_l;
+  // 32-channel groups (one 128-byte line per pixel), the last one masked when C % 32 == 16:
+  // 16-channel groups would split every line between two workgroups that run far apart
+#define DWT(KK, SS) dwt::launch<KK, SS, 8>(g, act, st);
+  if (k == 3 && s == 1) { DWT(3, 1) }
+  else if (k == 3) { DWT(3, 2) }
+  else if (k == 5 && s == 1) { DWT(5, 1) }
+  else { DWT(5, 2) }
+#undef DWT
+  return check_launch("dw_fwd_tile_kernel");
+}

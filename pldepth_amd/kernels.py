@@ -653,6 +653,22 @@ def dwconv_fwd(x, wdw, k, s, pad_t, pad_l, y, bn=None, act="none"):
                                 stream())
 
 
+def dwconv_fwd_bn_stats(x, wdw, k, s, pad_t, pad_l, y, ybn, bn=None, act="none", eps=1e-3,
+                        momentum=0.99):
+    """dwconv_fwd + the batch statistics of y for the BN after it: ybn = (mean, invstd,
+    moving_mean, moving_var) written like bn_stats (gathered in the tiled kernel's epilogue)."""
+    n, h, w, c = x.shape
+    _, oh, ow, _ = y.shape
+    need = lib().pld_dwconv_fwd_bn_stats_workspace_size(n, oh, ow, c, s)
+    ws = workspace(need, "bnstats")
+    mean, invstd, gamma, beta = bn if bn is not None else (None,) * 4
+    ym, yi, ymm, ymv = ybn
+    lib().pld_dwconv_fwd_bn_stats(ptr(x), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow,
+                                  ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ACT[act],
+                                  ptr(y), eps, momentum, ptr(ym), ptr(yi), ptr(ymm), ptr(ymv),
+                                  ptr(ws), need, stream())
+
+
 def dwconv_dgrad(dy, wdw, k, s, pad_t, pad_l, dx, accumulate=False):
     n, h, w, c = dx.shape
     _, oh, ow, _ = dy.shape

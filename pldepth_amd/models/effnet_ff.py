@@ -388,6 +388,9 @@ class EffNetFF:
         A, B, n = self.act, self.B, blk["name"]
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
         pt, pl = blk["pad"]
+        bn = blk["bn"]
+        rows = B * oh * ow
+        dwk = (self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl)
         if blk["ex"] != 1:
             ebn = blk["expand_bn"]
             self._conv_bn(K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
@@ -397,24 +400,26 @@ class EffNetFF:
             if training and n + "expand_activation" not in SKIP_TAPS:
                 # BN + swish fused into the depthwise conv's input read: the activation is
                 # never materialised (only the decoder's skip taps need it)
-                K.dwconv_fwd(A[n + "expand_pre"], self.frozen[blk["dw"]], blk["k"], blk["s"],
-                             pt, pl, A[n + "dw_pre"],
-                             bn=(ebn.mean, ebn.invstd, ebn.gamma, ebn.beta), act="swish")
+                src, pro = A[n + "expand_pre"], ebn
             else:
                 ebn.apply(A[n + "expand_pre"], B * h * w, "swish", A[n + "expand_activation"],
                           training)
-                K.dwconv_fwd(A[n + "expand_activation"], self.frozen[blk["dw"]], blk["k"],
-                             blk["s"], pt, pl, A[n + "dw_pre"])
+                src, pro = A[n + "expand_activation"], None
         elif x is None:  # block1a in training: the stem's pre-BN output through BN + swish
-            sbn = self.stem_bn
-            K.dwconv_fwd(A["stem_pre"], self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl,
-                         A[n + "dw_pre"], bn=(sbn.mean, sbn.invstd, sbn.gamma, sbn.beta),
-                         act="swish")
+            src, pro = A["stem_pre"], self.stem_bn
         else:
-            K.dwconv_fwd(x, self.frozen[blk["dw"]], blk["k"], blk["s"], pt, pl, A[n + "dw_pre"])
-        rows = B * oh * ow
-        bn = blk["bn"]
-        bn.stats_(A[n + "dw_pre"], rows, training)
+            src, pro = x, None
+        bnp = (pro.mean, pro.invstd, pro.gamma, pro.beta) if pro is not None else None
+        if training:
+            # the depthwise output's BN statistics gathered in the tiled kernel's epilogue
+            K.dwconv_fwd_bn_stats(src, *dwk, A[n + "dw_pre"],
+                                  (bn.mean, bn.invstd, bn.mmean, bn.mvar), bn=bnp,
+                                  act="swish" if pro is not None else "none", eps=bn.eps,
+                                  momentum=bn.momentum)
+        else:
+            K.dwconv_fwd(src, *dwk, A[n + "dw_pre"], bn=bnp,
+                         act="swish" if pro is not None else "none")
+            bn.stats_(A[n + "dw_pre"], rows, training)
         F = self.frozen
         se_w = (F[blk["se_w1"]].view(blk["cexp"], blk["cse"]), F[blk["se_b1"]],
                 F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]])

@@ -392,7 +392,11 @@ def test_residual_inplace_vector_and_scalar_paths(cuda, shape):
 @pytest.mark.parametrize("n,h,w,c,k,s", [(2, 12, 12, 16, 3, 1), (2, 12, 10, 24, 3, 2),
                                          (1, 14, 14, 40, 5, 2), (2, 7, 7, 8, 5, 1),
                                          (1, 13, 11, 4, 3, 2), (1, 9, 13, 12, 5, 1),
-                                         (2, 15, 17, 8, 5, 2), (1, 5, 6, 4, 3, 1)])
+                                         (2, 15, 17, 8, 5, 2), (1, 5, 6, 4, 3, 1),
+                                         # the LDS-tiled kernel (c % 16 == 0): 4- and 8-quad
+                                         # channel groups, ragged tiles, both strides
+                                         (2, 37, 21, 48, 5, 1), (1, 35, 19, 64, 3, 2),
+                                         (2, 18, 33, 32, 3, 1), (1, 17, 23, 96, 5, 2)])
 def test_dwconv(cuda, n, h, w, c, k, s):
     torch.manual_seed(k * 10 + s)
     x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
@@ -942,4 +946,36 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
     torch.cuda.synchronize()
     assert torch.equal(y, y_ref)
     for a, b in ((m, m_ref), (i, i_ref), (mm, mm_ref), (mv, mv_ref)):
+        assert rel_err(a, b) < 1e-6, rel_err(a, b)
+
+
+@pytest.mark.parametrize("n,h,w,c,k,s,pro", [(2, 37, 21, 48, 5, 1, True), (1, 35, 19, 64, 3, 2, True),
+                                             (2, 18, 33, 32, 3, 1, False),
+                                             (1, 9, 13, 12, 5, 1, True)])
+def test_dwconv_fwd_bn_stats(cuda, n, h, w, c, k, s, pro):
+    """pld_dwconv_fwd_bn_stats (the output's BN statistics from the tiled kernel's epilogue; the
+    c % 16 != 0 case through the register kernel + pld_bn_stats) == pld_dwconv_fwd_bn +
+    pld_bn_stats."""
+    g = torch.Generator(device=cuda).manual_seed(c * k + h)
+    x = torch.randn(n, h, w, c, device=cuda, generator=g)
+    wdw = torch.randn(k, k, c, device=cuda, generator=g) / k
+    bn = tuple(torch.rand(c, device=cuda, generator=g) + 0.5 for _ in range(4)) if pro else None
+    if s == 1:
+        pt = pl = (k - 1) // 2
+        oh, ow = h, w
+    else:
+        pt, pl = k // 2 - 1, k // 2
+        oh, ow = (h + 1) // 2, (w + 1) // 2
+    y_ref = torch.empty(n, oh, ow, c, device=cuda)
+    K.dwconv_fwd(x, wdw, k, s, pt, pl, y_ref, bn=bn, act="swish")
+    st_ref = [torch.empty(c, device=cuda), torch.empty(c, device=cuda),
+              torch.zeros(c, device=cuda), torch.ones(c, device=cuda)]
+    K.bn_stats(y_ref, n * oh * ow, c, *st_ref)
+    y = torch.empty_like(y_ref)
+    st = [torch.empty(c, device=cuda), torch.empty(c, device=cuda),
+          torch.zeros(c, device=cuda), torch.ones(c, device=cuda)]
+    K.dwconv_fwd_bn_stats(x, wdw, k, s, pt, pl, y, st, bn=bn, act="swish")
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    for a, b in zip(st, st_ref):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
