@@ -688,6 +688,7 @@ extern "C" int pld__x3_patch_ok(const GemmConvParams* p, int cfg);
 extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
 extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream);
+extern "C" int pld__x3_patch_wgrad_cw(int N);
 constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
@@ -1035,7 +1036,11 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
   if (kind == PLD_KIND_FP32) return "conv_igemm_kernel";
   if (pld_conv_schedule_class(a->math, a->tile) != PLD_SCHED_X3_PATCH) return "conv_x3_kernel";
   const int cfg = a->tile - 2 * pld__x3_num_cfg();
-  if (mode == 2) return wgrad_patch_geom(a) ? "conv_x3_patch_wgrad_kernel" : "conv_x3_kernel";
+  if (mode == 2)
+    return wgrad_patch_geom(a) ? (pld__x3_patch_wgrad_cw(a->cout) == 64
+                                      ? "conv_x3_patch_wgrad64_kernel"
+                                      : "conv_x3_patch_wgrad_kernel")
+                               : "conv_x3_kernel";
   // FWD view (dgrad: the input is dY, cout channels, one source)
   const int c1 = mode == 0 ? a->c1 : a->cout, c2 = mode == 0 ? a->c2 : 0;
   const bool geo = a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 &&
@@ -1198,9 +1203,10 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
     tile = -1;
   }
   if (patch_out) *patch_out = patch;
-  if (patch) {  // patch schedule: workgroups = chunks x 32-cout tiles x splits, ~512 in all
+  if (patch) {  // patch schedule: workgroups = chunks x cout tiles x splits, ~512 in all
     const long tiles = (long)cdiv(a->ow, 32) * cdiv(a->oh, 8) * a->n;
-    const long blocks = (long)(cdiv(a->c1, 32) + cdiv(a->c2, 32)) * cdiv(N, 32);
+    const long blocks = (long)(cdiv(a->c1, 32) + cdiv(a->c2, 32)) *
+                        cdiv(N, pld__x3_patch_wgrad_cw(N));
     long s = std::max<long>(1, (512 + blocks - 1) / blocks);
     s = std::min<long>(s, tiles);
     kt_per = (int)((tiles + s - 1) / s);

@@ -968,6 +968,178 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad_kernel(GemmConvParams
     }
 }
 
+// The same for 64 output channels per workgroup (N > 32: the 240- and 144-wide decoder convs):
+// the input patch of a tile is staged ONCE for both 32-wide cout tiles (the 32-wide kernel
+// re-stages it per cout tile: 8 / 5 times for N = 240 / 144 — fetch-bound, PMC: 2.9x the
+// algorithmic bytes). 768 threads = 12 waves = 2 cout tiles x 3 tap rows (ty) x 2 row halves:
+// a wave accumulates the 3 taps (ty, 0..2) of one cout tile over 4 output rows (8 pixel
+// k-steps): 48 accumulator VGPRs, 3 waves per SIMD. One LDS stage (patch 43.5 KB + the
+// [256 px][64 co] dY image 64 KB) with the next tile's global loads held in registers during the
+// MFMAs. dY rows are 128 B: the 32-byte column blocks are XOR-swizzled by 2 ((row >> 1) & 1) so
+// the transposed reads of 4 consecutive rows hit 4 distinct bank ranges. The two row halves are
+// summed through LDS at the end (fixed order).
+constexpr int PW_B64 = PT_H * PT_W * 128;     // dY image plane: [256 pixels][64 co] bf16
+constexpr int PW64_STAGE = 2 * PW_A + 2 * PW_B64;
+constexpr int PW64_RED = 6 * 3 * 64 * 16 * 4;   // 6 slots of 3 tiles x 64 lanes x 16 floats
+constexpr int PW64_SMEM = PW64_STAGE > PW64_RED ? PW64_STAGE : PW64_RED;
+constexpr int PW64_T = 768;
+
+__device__ __forceinline__ int dy64_off(int k, int col) {  // byte offset of (row k, cout col)
+  return k * 128 + (((col >> 4) ^ (((k >> 1) & 1) << 1)) << 5) + (col & 15) * 2;
+}
+
+__device__ __forceinline__ bf16x8 tr_frag_dy64(const unsigned char* plane, int row0, int c0,
+                                               int lane) {
+  const int i16 = lane & 15, grp = (lane >> 4) & 1, h = lane >> 5;
+  const int r = row0 + 8 * h + (i16 >> 2);
+  const int col = c0 + 16 * grp + 4 * (i16 & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + dy64_off(r, col)));
+  const v4s hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + dy64_off(r + 4, col)));
+  const v4s v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(PW64_T) void conv_x3_patch_wgrad64_kernel(GemmConvParams p,
+                                                                       int tiles,
+                                                                       int tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[PW64_SMEM];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  const bool s2 = q >= p.kc1;
+  const int cb = (s2 ? q - p.kc1 : q) * 32;
+  const int cs = s2 ? p.c2 : p.c1;
+  const int nv = min(32, cs - cb);
+  const int n0 = nb * 64;
+  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
+  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
+  const long img_in = (long)p.h * p.w * cs;
+  const float* xsrc = s2 ? p.x2 : p.x1;
+  unsigned char* A = smem;
+  unsigned char* B = smem + 2 * PW_A;
+
+  constexpr int EA = P_PIX * 8, IA = (EA + PW64_T - 1) / PW64_T;    // patch: 4-channel quads
+  constexpr int EB = PT_H * PT_W * 16, IB = (EB + PW64_T - 1) / PW64_T;  // dY: 4-cout quads
+  float4 va[IA], vb[IB];
+  auto load = [&](int t) {
+    const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
+    const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + PW64_T * i;
+      const int px = e >> 3, c4 = (e & 7) * 4;
+      const int py = px / P_W, pxx = px - py * P_W;
+      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+      const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
+                      (unsigned)ix < (unsigned)p.w;
+      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
+    }
+    const long img_out = (long)p.oh * p.ow;
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + PW64_T * i;
+      const int k = e >> 4, c4 = (e & 15) * 4;
+      const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
+      const bool ok = e < EB && oy < p.oh && ox < p.ow && n0 + c4 < p.N;
+      vb[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int e = threadIdx.x + PW64_T * i;
+      if (e < EA) {
+        unsigned h0, l0, h1, l1;
+        split2(va[i].x, va[i].y, h0, l0);
+        split2(va[i].z, va[i].w, h1, l1);
+        const int o = (e >> 3) * 64 + (e & 7) * 8;
+        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(A + PW_A + o) = u32x2{l0, l1};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int e = threadIdx.x + PW64_T * i;
+      if (e < EB) {
+        unsigned h0, l0, h1, l1;
+        split2(vb[i].x, vb[i].y, h0, l0);
+        split2(vb[i].z, vb[i].w, h1, l1);
+        const int o = dy64_off(e >> 4, (e & 15) * 4);
+        *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(B + PW_B64 + o) = u32x2{l0, l1};
+      }
+    }
+  };
+
+  const int ct = wave / 6, ty = (wave % 6) >> 1, rh = wave & 1;
+  floatx16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  if (t_begin < t_end) {
+    load(t_begin);
+    store();
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      if (t + 1 < t_end) load(t + 1);  // in flight under the MFMAs
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 4 * rh + rr;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int k0 = 32 * row + 16 * s;
+          const bf16x8 bh = tr_frag_dy64(B, k0, 32 * ct, lane);
+          const bf16x8 bl = tr_frag_dy64(B + PW_B64, k0, 32 * ct, lane);
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int r0 = (row + ty) * P_W + 16 * s + tx;
+            const bf16x8 ah = tr_frag_rows(A, r0, lane), al = tr_frag_rows(A + PW_A, r0, lane);
+            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tx], 0, 0, 0);
+            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tx], 0, 0, 0);
+            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tx], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();  // every wave is done with this tile's LDS
+      if (t + 1 < t_end) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+  // the two row halves of each (cout tile, tap row): rh 1 -> rh 0 through LDS
+  float* slot = reinterpret_cast<float*>(smem) + (long)(wave >> 1) * 3 * 64 * 16;
+  if (rh == 1) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) slot[(t * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (rh == 1) return;
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] += slot[(t * 16 + r) * 64 + lane];
+  const int h = lane >> 5, col = n0 + 32 * ct + (lane & 31);
+  if (col >= p.N) return;
+  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ci >= nv) continue;
+      const long m = (long)(ty * 3 + tx) * p.C + (s2 ? p.c1 : 0) + cb + ci;
+      float* dst = out + m * p.N + col;
+      *dst = (p.zstride == 0 && p.acc1) ? *dst + acc[tx][r] : acc[tx][r];
+    }
+}
+
 // ------------------------------------------------------------------------ schedules
 struct Cfg { int bm, bn, tm, tn, occ; };
 // occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
@@ -1097,6 +1269,13 @@ extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p) {
 extern "C" int pld__x3_patch_wgrad_tiles(const GemmConvParams* p) {
   return (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, x3::PT_H) * p->n);
 }
+// output channels per workgroup of the patch WGRAD kernel: 64 (one staged patch feeds two
+// 32-wide cout tiles) where that pads no more MFMA columns than 32-wide tiles do (N = 240: 256
+// either way, dec1 wgrad 0.66 -> 0.56 ms); N = 144 keeps 32 (192 vs 160 padded: no gain)
+extern "C" int pld__x3_patch_wgrad_cw(int N) {
+  return (N > 32 && 2 * cdiv(N, 64) == cdiv(N, 32)) ? 64 : 32;
+}
+
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream) {
   if (!pld__x3_patch_wgrad_ok(p) || splits < 1) {
     set_error("conv_x3_patch_wgrad: ineligible geometry");
@@ -1106,6 +1285,11 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
   const int tps = (int)cdiv(tiles, splits);
   p->kc1 = (int)cdiv(p->c1, 32);
   const int chunks = p->kc1 + (int)cdiv(p->c2, 32);
+  if (pld__x3_patch_wgrad_cw(p->N) == 64) {
+    dim3 grid(chunks, cdiv(p->N, 64), cdiv(tiles, tps));
+    x3::conv_x3_patch_wgrad64_kernel<<<grid, x3::PW64_T, 0, as_stream(stream)>>>(*p, tiles, tps);
+    return check_launch("conv_x3_patch_wgrad64_kernel");
+  }
   dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
   x3::conv_x3_patch_wgrad_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
   return check_launch("conv_x3_patch_wgrad_kernel");

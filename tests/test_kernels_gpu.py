@@ -186,7 +186,10 @@ def test_conv_fwd_dgrad_wgrad(cuda, case, math):
                                   # 8 x 32 tiles, N = 72: two N tiles at BN 64), dgrad with
                                   # dY of 32 channels routed to a 48 | 24 concat
                                   (2, 13, 40, 32, 0, 3, 1, 72, True),
-                                  (2, 11, 35, 48, 24, 3, 1, 32, True)])
+                                  (2, 11, 35, 48, 24, 3, 1, 32, True),
+                                  # the 64-cout patch WGRAD (dec1-like: concat of 32-channel
+                                  # chunks with a ragged 16-channel one, N = 240, 28 x 28)
+                                  (2, 28, 28, 64, 48, 3, 1, 240, False)])
 def test_conv_every_schedule(cuda, case, math):
     """Each tile x split-K schedule computes the same conv (fwd with bias routing, dgrad into
     two concat destinations with accumulate)."""
