@@ -675,6 +675,17 @@ extern "C" int pld__thin_geom(const pld_conv_args* a);
 extern "C" int pld__thin_gemm(const float* a, const float* b, const float* bias, float* out,
                               long M, int K, int N, int acc, void* stream, double* stats);
 extern "C" int pld__thin_stats_parts(long M);
+// wide1x1.hip: streaming bf16x3 1x1 GEMM for short reductions into wide outputs
+extern "C" int pld__wide_ok(int K, int N);
+extern "C" int pld__wide_stats_parts(long M, int K, int N);
+extern "C" int pld__wide_gemm(const float* a, const float* w, const float* bias, float* out,
+                              long M, int K, int N, int acc, void* stream, double* stats);
+// a bf16x3 1x1 conv whose GEMM (fwd K = cin, N = cout; dgrad K = cout, N = cin) takes the wide
+// kernel: unstrided single-source geometry that the exact thin kernel does not cover
+static bool wide_conv(const pld_conv_args* a, int K, int N) {
+  return a->math == PLD_MATH_BF16X3 && pld__thin_geom(a) && !pld__thin_ok(K, N) &&
+         pld__wide_ok(K, N) && aligned16(a->x1);
+}
 // bn.hip: BN batch statistics from channel-major fp64 partials (stats_finalize_kernel)
 extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows, int c,
                                     float eps, float momentum, float* mean, float* invstd,
@@ -925,6 +936,9 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
       aligned16(w_ohwi))
     return pld__thin_gemm(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, a->c1, a->cout,
                           accumulate, stream, nullptr);
+  if (wide_conv(a, a->c1, a->cout) && aligned16(w_ohwi) && aligned16(y))
+    return pld__wide_gemm(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, a->c1, a->cout,
+                          accumulate, stream, nullptr);
   p.bmat = w_ohwi;
   p.bsplit = (const float*)a->w_split;
   p.M = a->n * a->oh * a->ow;
@@ -944,18 +958,26 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
 }
 
 // conv forward + the batch statistics of its output for the BatchNormalization that follows:
-// where the kernel the conv runs on can gather them as it stores its tile (thin 1x1), the
-// output is not read back; otherwise pld_conv2d_fwd + pld_bn_stats.
-static bool fwd_stats_fused(const pld_conv_args* a, const float* w_ohwi, const float* y) {
+// where the kernel the conv runs on can gather them as it stores its tile (thin and wide 1x1),
+// the output is not read back; otherwise pld_conv2d_fwd + pld_bn_stats.
+static bool fwd_stats_thin(const pld_conv_args* a, const float* w_ohwi, const float* y) {
   return !pld__skinny_eligible(a) && pld__thin_geom(a) && pld__thin_ok(a->c1, a->cout) &&
          aligned16(a->x1) && aligned16(y) && aligned16(w_ohwi);
+}
+static bool fwd_stats_wide(const pld_conv_args* a, const float* w_ohwi, const float* y) {
+  return !pld__skinny_eligible(a) && wide_conv(a, a->c1, a->cout) && aligned16(w_ohwi) &&
+         aligned16(y);
 }
 
 extern "C" size_t pld_conv2d_fwd_bn_stats_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->oh <= 0 || a->ow <= 0 || a->cout <= 0) return 0;
   const long rows = (long)a->n * a->oh * a->ow;
-  const size_t fused = sizeof(double) * 2 * (size_t)a->cout * pld__thin_stats_parts(rows);
-  return std::max(fused, pld_channel_reduce_workspace_size(rows, a->cout));
+  const size_t thin = sizeof(double) * 2 * (size_t)a->cout * pld__thin_stats_parts(rows);
+  const size_t wide = pld__wide_ok(a->c1, a->cout)
+                          ? sizeof(double) * 2 * (size_t)a->cout *
+                                pld__wide_stats_parts(rows, a->c1, a->cout)
+                          : 0;
+  return std::max(std::max(thin, wide), pld_channel_reduce_workspace_size(rows, a->cout));
 }
 
 extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_ohwi,
@@ -969,13 +991,21 @@ extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_oh
   PLD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr),
                 "pld_conv2d_fwd_bn_stats: moving_mean/moving_var must both be given or both NULL");
   const long rows = (long)a->n * a->oh * a->ow;
-  if (fwd_stats_fused(a, w_ohwi, y)) {
+  if (fwd_stats_thin(a, w_ohwi, y)) {
     int rc = pld__thin_gemm(a->x1, w_ohwi, bias, y, rows, a->c1, a->cout, 0, stream,
                             (double*)ws);
     if (rc) return rc;
     return pld__bn_stats_finish((const double*)ws, pld__thin_stats_parts(rows), rows, a->cout,
                                 eps, momentum, mean, invstd, moving_mean, moving_var,
                                 as_stream(stream));
+  }
+  if (fwd_stats_wide(a, w_ohwi, y)) {
+    int rc = pld__wide_gemm(a->x1, w_ohwi, bias, y, rows, a->c1, a->cout, 0, stream,
+                            (double*)ws);
+    if (rc) return rc;
+    return pld__bn_stats_finish((const double*)ws, pld__wide_stats_parts(rows, a->c1, a->cout),
+                                rows, a->cout, eps, momentum, mean, invstd, moving_mean,
+                                moving_var, as_stream(stream));
   }
   int rc = pld_conv2d_fwd(a, w_ohwi, bias, y, 0, stream);
   if (rc) return rc;
@@ -1008,6 +1038,8 @@ extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
   if (mode != 2 && pld__thin_geom(a) &&
       (mode == 0 ? pld__thin_ok(a->c1, a->cout) : pld__thin_ok(a->cout, a->c1)))
     return PLD_KIND_DIRECT;
+  if (mode != 2 && (mode == 0 ? wide_conv(a, a->c1, a->cout) : wide_conv(a, a->cout, a->c1)))
+    return PLD_KIND_DIRECT;
   bool geom, x3;
   int t;
   if (mode == 2)
@@ -1031,6 +1063,8 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
     if (pld__skinny_eligible(a))
       return mode == 0 ? "skinny_fwd_kernel" : mode == 1 ? "skinny_dgrad_kernel"
                                                          : "skinny_wgrad_kernel";
+    if (mode == 0 ? wide_conv(a, a->c1, a->cout) : wide_conv(a, a->cout, a->c1))
+      return "wide1x1_kernel";
     return "thin1x1_kernel";
   }
   if (kind == PLD_KIND_FP32) return "conv_igemm_kernel";
@@ -1144,6 +1178,9 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
   if (pld__thin_geom(a) && pld__thin_ok(a->cout, a->c1) && aligned16(dy) && aligned16(dx1) &&
       aligned16(w_dgrad))
     return pld__thin_gemm(dy, w_dgrad, nullptr, dx1, (long)a->n * a->h * a->w, a->cout, a->c1,
+                          accumulate1, stream, nullptr);
+  if (wide_conv(a, a->cout, a->c1) && aligned16(dy) && aligned16(w_dgrad) && aligned16(dx1))
+    return pld__wide_gemm(dy, w_dgrad, nullptr, dx1, (long)a->n * a->h * a->w, a->cout, a->c1,
                           accumulate1, stream, nullptr);
   // dx[img][iy][ix][ci] = sum_{ty,tx,co} dy[img][iy+ty-pt'][ix+tx-pl'][co] * Wd[ci][ty][tx][co]
   // with pt' = kh-1-pt and the output spatial = the forward input spatial.

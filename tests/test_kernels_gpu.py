@@ -952,6 +952,55 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 20, 17, 40, 240), (1, 13, 11, 112, 672),
+                                            (3, 7, 9, 80, 480), (1, 6, 5, 8, 520),
+                                            (2, 9, 9, 128, 1152), (1, 3, 7, 56, 200)])
+def test_wide1x1(cuda, n, h, w, cin, cout):
+    """The streaming bf16x3 1x1 kernel (wide1x1.hip: K <= 128 reductions into wide outputs):
+    fwd (+bias, +accumulate), dgrad (the transposed GEMM, +accumulate) and the BN statistics of
+    its epilogue against fp64; ragged strips (rows % 32 != 0) and column tiles (N % 32 != 0)."""
+    lib = K.lib()
+    g = torch.Generator(device=cuda).manual_seed(cin + cout + h)
+    x = torch.randn(n, h, w, cin, device=cuda, generator=g)
+    wt = torch.randn(1, 1, cin, cout, device=cuda, generator=g) / cin ** 0.5
+    b = torch.randn(cout, device=cuda, generator=g)
+    wn = K.filter_to_native(wt)
+    args = K.conv_args(x, None, 1, 1, 1, 0, 0, h, w, cout, math="bf16x3")
+    assert lib.pld_conv_kernel_name(C.byref(args), 0) == b"wide1x1_kernel"
+    ref = (x.double().reshape(-1, cin) @ wt.double().reshape(cin, cout) + b.double())
+    y = torch.empty(n, h, w, cout, device=cuda)
+    K.conv2d_fwd(args, wn, b, y)
+    torch.cuda.synchronize()
+    assert rel_err(y.reshape(-1, cout), ref) < 2e-5
+    K.conv2d_fwd(args, wn, b, y, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(y.reshape(-1, cout), 2 * ref) < 2e-5
+    # BN statistics from the epilogue
+    y2 = torch.empty_like(y)
+    m, i = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+    mm, mv = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+    K.conv2d_fwd_bn_stats(args, wn, None, y2, m, i, mm, mv)
+    r2 = x.double().reshape(-1, cin) @ wt.double().reshape(cin, cout)
+    torch.cuda.synchronize()
+    assert rel_err(y2.reshape(-1, cout), r2) < 2e-5
+    m_ref, i_ref = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+    K.bn_stats(y2, n * h * w, cout, m_ref, i_ref)
+    torch.cuda.synchronize()
+    assert rel_err(m, m_ref) < 1e-5 and rel_err(i, i_ref) < 1e-5
+    # dgrad of a cout -> cin 1x1 conv runs the same GEMM with K = cout: build it the other way
+    dy = torch.randn(n, h, w, cin, device=cuda, generator=g)
+    wt2 = torch.randn(1, 1, cout, cin, device=cuda, generator=g) / cin ** 0.5  # fwd cout->cin
+    wd = K.filter_to_dgrad(wt2)
+    dargs = K.conv_args(torch.empty(n, h, w, cout, device=cuda), None, 1, 1, 1, 0, 0, h, w, cin,
+                        math="bf16x3")
+    assert lib.pld_conv_kernel_name(C.byref(dargs), 1) == b"wide1x1_kernel"
+    dx = torch.full((n, h, w, cout), 0.5, device=cuda)
+    K.conv2d_dgrad(dargs, dy, wd, dx, acc1=True)
+    dref = dy.double().reshape(-1, cin) @ wt2.double().reshape(cout, cin).t() + 0.5
+    torch.cuda.synchronize()
+    assert rel_err(dx.reshape(-1, cout), dref) < 2e-5
+
+
 @pytest.mark.parametrize("n,h,w,c,k,s,pro", [(2, 37, 21, 48, 5, 1, True), (1, 35, 19, 64, 3, 2, True),
                                              (2, 18, 33, 32, 3, 1, False),
                                              (1, 9, 13, 12, 5, 1, True)])
