@@ -188,6 +188,14 @@ int pld_filter_to_native(const float* w_hwio, int kh, int kw, int cin, int cout,
 /* HWIO -> dgrad native [cin][kh][kw][cout] with flipped taps (kh-1-i, kw-1-j) */
 int pld_filter_to_dgrad(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_dgrad,
                         void* stream);
+/* Per-step refresh of a trainable conv's filter copies after the optimizer (replaces the
+ * Keras variable read of pl_hourglass.py:56-96's decoder Conv2D kernels): forward native
+ * [cout][kh][kw][cin] and, if w_dgrad is given, the flipped dgrad [cin][kh][kw][cout], each with
+ * its bf16x3 split (pld_filter_split layout) when the split pointer is non-NULL — the same
+ * bytes as pld_filter_to_native + pld_filter_to_dgrad + pld_filter_split, in two coalesced
+ * passes (a 64x64 LDS-tiled transpose and a row permutation). */
+int pld_filter_refresh(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_ohwi,
+                       void* w_ohwi_split, float* w_dgrad, void* w_dgrad_split, void* stream);
 
 /* per-channel column sum over `rows` rows of an [rows][c] tensor: out[c] (+)= sum_r x[r][c]
  * (bias gradient of Conv2D). ws >= pld_channel_reduce_workspace_size(rows, c). */

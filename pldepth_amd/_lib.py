@@ -62,6 +62,7 @@ _SIGS = {
     "pld_filter_to_native": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_filter_split": (I32, [P, I64, I32, P, P]),
     "pld_filter_to_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
+    "pld_filter_refresh": (I32, [P, I32, I32, I32, I32, P, P, P, P, P]),
     "pld_channel_reduce_workspace_size": (SZ, [I64, I32]),
     "pld_channel_sum": (I32, [P, I64, I32, P, I32, P, P]),
     "pld_bn_stats": (I32, [P, I64, I32, F32, F32, P, P, P, P, P, P]),

@@ -560,6 +560,84 @@ __global__ void filter_dgrad_kernel(const float* __restrict__ w, int kh, int kw,
   }
 }
 
+// ---- per-step filter refresh (trainable convs after the optimizer): both native layouts and
+// their bf16x3 splits from the HWIO weights in two coalesced passes
+typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
+
+// 8 fp32 -> the pld_filter_split chunk: 8 bf16 hi then 8 bf16 lo (conv_x3.hip's split2)
+__device__ __forceinline__ void split_chunk(const float* v, u32x4r* out) {
+  unsigned hs[4], ls[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 h0 = (__bf16)v[2 * i], h1 = (__bf16)v[2 * i + 1];
+    const __bf16 l0 = (__bf16)(v[2 * i] - (float)h0), l1 = (__bf16)(v[2 * i + 1] - (float)h1);
+    hs[i] = __builtin_bit_cast(unsigned short, h0) |
+            (unsigned)__builtin_bit_cast(unsigned short, h1) << 16;
+    ls[i] = __builtin_bit_cast(unsigned short, l0) |
+            (unsigned)__builtin_bit_cast(unsigned short, l1) << 16;
+  }
+  out[0] = u32x4r{hs[0], hs[1], hs[2], hs[3]};
+  out[1] = u32x4r{ls[0], ls[1], ls[2], ls[3]};
+}
+
+// HWIO viewed as W[R = taps*cin][cout] -> native O[cout][R]: 64x64 tiles transposed through LDS
+// (row pitch 65: conflict-free both ways); every output lane writes one 8-value chunk (32 B of
+// fp32 + its 32-B split). R % 8 == 0.
+__global__ __launch_bounds__(256) void filter_native_tiled_kernel(const float* __restrict__ w,
+                                                                  int R, int cout,
+                                                                  float* __restrict__ o,
+                                                                  u32x4r* __restrict__ osplit) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, lc = tid & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = (tid >> 6) + 4 * i, gr = r0 + r, gc = c0 + lc;
+    t[lc][r] = (gr < R && gc < cout) ? w[(long)gr * cout + gc] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i, c = e >> 3, q = e & 7;
+    const int gc = c0 + c, gr = r0 + 8 * q;
+    if (gc < cout && gr < R) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = t[c][8 * q + j];
+      const long f = (long)gc * R + gr;
+      reinterpret_cast<float4*>(o + f)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(o + f)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      if (osplit) split_chunk(v, osplit + f / 4);
+    }
+  }
+}
+
+// HWIO -> dgrad [cin][taps'][cout] (taps flipped): a permutation of cout-long rows, one 8-value
+// chunk per thread (coalesced both sides). cout % 8 == 0.
+__global__ __launch_bounds__(256) void filter_dgrad_rows_kernel(const float* __restrict__ w,
+                                                                int taps, int cin, int cout,
+                                                                float* __restrict__ o,
+                                                                u32x4r* __restrict__ osplit) {
+  const int c8n = cout >> 3;
+  const long n = (long)cin * taps * c8n;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(e % c8n);
+    const long rest = e / c8n;
+    const int tp = (int)(rest % taps), ci = (int)(rest / taps);
+    const float4* src = reinterpret_cast<const float4*>(
+        w + ((long)(taps - 1 - tp) * cin + ci) * cout + 8 * c8);
+    const float4 a = src[0], b = src[1];
+    const long f = ((long)ci * taps + tp) * cout + 8 * c8;
+    reinterpret_cast<float4*>(o + f)[0] = a;
+    reinterpret_cast<float4*>(o + f)[1] = b;
+    if (osplit) {
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      split_chunk(v, osplit + f / 4);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------ dispatch
 // ---- tile configurations and a small cost model ----
 // (BM, BN, WM, WN): 4 waves; each wave computes (BM/WM) x (BN/WN) as 32x32 MFMA tiles.
@@ -922,6 +1000,40 @@ extern "C" int pld_filter_to_dgrad(const float* w_hwio, int kh, int kw, int cin,
   filter_dgrad_kernel<<<std::min<unsigned>(cdiv(n, 256), 4096), 256, 0, as_stream(stream)>>>(
       w_hwio, kh, kw, cin, cout, w_dgrad);
   return check_launch("filter_dgrad_kernel");
+}
+
+extern "C" int pld_filter_refresh(const float* w_hwio, int kh, int kw, int cin, int cout,
+                                  float* w_ohwi, void* w_ohwi_split, float* w_dgrad,
+                                  void* w_dgrad_split, void* stream) {
+  PLD_CHECK_ARG(w_hwio && w_ohwi && kh > 0 && kw > 0 && cin > 0 && cout > 0,
+                "pld_filter_refresh: bad args");
+  PLD_CHECK_ARG(!w_dgrad_split || w_dgrad, "pld_filter_refresh: dgrad split without dgrad");
+  hipStream_t st = as_stream(stream);
+  const int taps = kh * kw;
+  const long R = (long)taps * cin;
+  int rc;
+  if (R % 8 == 0 && aligned16(w_ohwi) && (!w_ohwi_split || aligned16(w_ohwi_split)) &&
+      R < (1L << 30)) {
+    const dim3 grid((unsigned)cdiv(R, 64), (unsigned)cdiv(cout, 64));
+    filter_native_tiled_kernel<<<grid, 256, 0, st>>>(w_hwio, (int)R, cout, w_ohwi,
+                                                     (u32x4r*)w_ohwi_split);
+    rc = check_launch("filter_native_tiled_kernel");
+  } else {
+    rc = pld_filter_to_native(w_hwio, kh, kw, cin, cout, w_ohwi, stream);
+    if (!rc && w_ohwi_split) rc = pld_filter_split(w_ohwi, cout, (int)R, w_ohwi_split, stream);
+  }
+  if (rc || !w_dgrad) return rc;
+  const long n = (long)cin * taps * cout;
+  if (cout % 8 == 0 && aligned16(w_hwio) && aligned16(w_dgrad) &&
+      (!w_dgrad_split || aligned16(w_dgrad_split))) {
+    filter_dgrad_rows_kernel<<<std::min<unsigned>(cdiv(n / 8, 256), 8192), 256, 0, st>>>(
+        w_hwio, taps, cin, cout, w_dgrad, (u32x4r*)w_dgrad_split);
+    return check_launch("filter_dgrad_rows_kernel");
+  }
+  rc = pld_filter_to_dgrad(w_hwio, kh, kw, cin, cout, w_dgrad, stream);
+  if (!rc && w_dgrad_split)
+    rc = pld_filter_split(w_dgrad, cin, taps * cout, w_dgrad_split, stream);
+  return rc;
 }
 
 extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,

@@ -341,6 +341,18 @@ def _splitk_ws(args, fn):
         args.ws, args.ws_bytes = None, 0
 
 
+def filter_refresh(w_hwio, w_nat, w_nat_split=None, w_dg=None, w_dg_split=None):
+    """pld_filter_refresh: native (+ split) and dgrad (+ split) filter copies of an HWIO weight in
+    two passes; the split copies are attached to their fp32 tensors (as filter_split does)."""
+    kh, kw, cin, cout = w_hwio.shape
+    lib().pld_filter_refresh(ptr(w_hwio), kh, kw, cin, cout, ptr(w_nat), ptr(w_nat_split),
+                             ptr(w_dg), ptr(w_dg_split), stream())
+    if w_nat_split is not None:
+        w_nat._pld_split = w_nat_split
+    if w_dg_split is not None:
+        w_dg._pld_split = w_dg_split
+
+
 def filter_split(w, out=None):
     """Split a [rows][K] fp32 filter (K % 8 == 0) for the bf16x3 kernel and attach the copy to
     the fp32 tensor object (w._pld_split): conv2d_fwd / conv2d_dgrad given that same tensor use

@@ -150,10 +150,4 @@ class _Conv:
                         if self.w_dg is not None and self.cout % 8 == 0 else None)
 
     def refresh(self):
-        K.filter_to_native(self.w, self.w_nat)
-        if self.w_nat_x3 is not None:
-            K.filter_split(self.w_nat, self.w_nat_x3)
-        if self.w_dg is not None:
-            K.filter_to_dgrad(self.w, self.w_dg)
-            if self.w_dg_x3 is not None:
-                K.filter_split(self.w_dg, self.w_dg_x3)
+        K.filter_refresh(self.w, self.w_nat, self.w_nat_x3, self.w_dg, self.w_dg_x3)

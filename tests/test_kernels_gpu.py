@@ -1031,3 +1031,26 @@ def test_dwconv_fwd_bn_stats(cuda, n, h, w, c, k, s, pro):
     assert torch.equal(y, y_ref)
     for a, b in zip(st, st_ref):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
+
+
+@pytest.mark.parametrize("kh,cin,cout", [(3, 1952, 672), (3, 912, 240), (3, 32, 1), (1, 40, 240),
+                                         (3, 12, 20), (3, 72, 100)])
+def test_filter_refresh(cuda, kh, cin, cout):
+    """pld_filter_refresh (tiled transpose + row permutation, splits written beside the fp32
+    copies; generic kernels where the shapes are not 8-aligned) == pld_filter_to_native +
+    pld_filter_to_dgrad + pld_filter_split, bit for bit."""
+    g = torch.Generator(device=cuda).manual_seed(kh * cin + cout)
+    w = torch.randn(kh, kh, cin, cout, device=cuda, generator=g)
+    nat_ref = K.filter_to_native(w)
+    dg_ref = K.filter_to_dgrad(w)
+    nat, dg = torch.empty_like(nat_ref), torch.empty_like(dg_ref)
+    ns = torch.empty_like(nat_ref) if (kh * kh * cin) % 8 == 0 else None
+    ds = torch.empty_like(dg_ref) if (kh * kh * cout) % 8 == 0 else None
+    K.filter_refresh(w, nat, ns, dg, ds)
+    torch.cuda.synchronize()
+    assert torch.equal(nat, nat_ref) and torch.equal(dg, dg_ref)
+    if ns is not None:
+        assert torch.equal(ns, K.filter_split(nat_ref)) and nat._pld_split is ns
+    if ds is not None:
+        assert torch.equal(ds, K.filter_split(dg_ref))
+    torch.cuda.synchronize()
