@@ -135,6 +135,23 @@ def profile_conv(trainer, lr):
     return [(n, k, m, f, b, e0.elapsed_time(e1) / 1e3) for n, k, m, f, b, e0, e1 in recs]
 
 
+def attach_traffic(roof, path, workload):
+    """roofline.traffic = HBM bytes per launch of the dominant kernel from the committed PMC
+    profile (tools/dominant_traffic.py), only when that profile measured the same kernel on the
+    same workload; otherwise it stays null."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return
+    if t.get("kernel") != roof["kernel"] or (workload and t.get("workload") != workload):
+        roof["traffic_note"] = "profile does not match this run's dominant kernel / workload"
+        return
+    roof["traffic"] = t["hbm_bytes_per_launch"]
+    roof["traffic_algorithmic"] = t["algorithmic_bytes_per_launch"]
+    roof["traffic_over_algorithmic"] = t["hbm_over_algorithmic"]
+
+
 def conv_roofline(recs, traffic_profile=None):
     """roofline object. Top level = the DOMINANT kernel (the conv kernel name with the largest
     summed time in the profiled step): achieved = its algorithmic FLOPs / its measured time, peak
@@ -353,8 +370,10 @@ def main():
                     help="conv arithmetic policy (kernels.conv_policy): auto = decoder bf16x3, "
                          "encoder bf16x3 where the BN sees >= 4096 values per channel (all of "
                          "them at 448x448 batch 32); mixed = encoder fp32, decoder bf16x3")
-    ap.add_argument("--traffic-profile", default="profiles/r02_pmc_dominant.txt",
-                    help="committed PMC summary of the dominant kernel (named in the line)")
+    ap.add_argument("--traffic-profile", default="profiles/r02_pmc_dominant.json",
+                    help="PMC traffic of the dominant kernel (tools/dominant_traffic.py, committed "
+                         "from the same HEAD and workload): fills roofline.traffic when its kernel "
+                         "and workload match this run's")
     ap.add_argument("--tile-cache", default="",
                     help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
@@ -391,6 +410,9 @@ def main():
     recs = profile_conv(tr, 0.01)
     flops_img = tr.engine.conv_flops_per_image()
     roof = conv_roofline(recs, a.traffic_profile)
+    workload = (f"{a.model} train step {H}x{H}, per-GPU batch {B}, ranking_size {L}, "
+                f"rankings_per_image {R}, sampler {tr.strategy}, Adam-AMSGrad")
+    attach_traffic(roof, a.traffic_profile, workload)
     roof["step_frac"] = round(value / world * flops_img / 1e12 / roof["family"]["peak"], 4)
     out = {
         "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
@@ -406,9 +428,7 @@ def main():
         "dtype": "fp32 (bf16x3 MFMA)",
         "data": "synthetic (U[0,1) RGB, smooth 8-bit depth, Bernoulli(0.9) mask; Keras-default "
                 "random-init weights)",
-        "config": {"workload": f"{a.model} train step {H}x{H}, per-GPU batch {B}, "
-                               f"ranking_size {L}, rankings_per_image {R}, "
-                               f"sampler {tr.strategy}, Adam-AMSGrad",
+        "config": {"workload": workload,
                    "model": a.model, "global_batch": world * B, "input": f"{H}x{H}",
                    "ranking_size": L, "rankings_per_image": R,
                    "parallelism": f"dp{world}", "graph": not a.no_graph},
