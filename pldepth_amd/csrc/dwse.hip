@@ -585,8 +585,8 @@ __global__ __launch_bounds__(SE_THREADS) void se_fc_bwd_kernel(const double* __r
 static unsigned grid_for(long n) { return std::min<unsigned>(std::max(cdiv(n, 256), 1u), 8192); }
 
 static int se_rsplit(int n, int hw, int c) {
-  const int cy = (int)cdiv(c / 4, 256);
-  int rs = (int)std::max(1L, 1024L / ((long)n * cy));
+  const int cy = std::max(1, (int)cdiv(c / 4, 256));  // c < 4: one group (found by tools/asan)
+  int rs = (int)std::max(1L, 1024L / ((long)std::max(n, 1) * cy));
   rs = std::min(rs, std::max(1, hw / 32));
   return rs;
 }
