@@ -112,14 +112,45 @@ def up2(x):
     return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
 
 
+def bn_infer(x, gamma, beta, mmean, mvar, eps=BN_EPS):
+    """Keras BatchNormalization(training=False): the moving statistics."""
+    v = lambda t: t.view(1, -1, 1, 1)
+    return (x - v(mmean)) / torch.sqrt(v(mvar) + eps) * v(gamma) + v(beta)
+
+
+_TRAINING = [True]
+_STATS = [None]  # forward(bn_stats=...): {bn name: (batch mean, biased batch variance)}
+
+
 def _bn(P, name, x):
-    return bn_train(x, P[name + "/gamma"], P[name + "/beta"])
+    if _TRAINING[0]:
+        if _STATS[0] is not None:
+            m = x.mean(dim=(0, 2, 3))
+            _STATS[0][name] = (m, ((x - m.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3)))
+        return bn_train(x, P[name + "/gamma"], P[name + "/beta"])
+    return bn_infer(x, P[name + "/gamma"], P[name + "/beta"], P[name + "/moving_mean"],
+                    P[name + "/moving_variance"])
 
 
-def forward(P, x_nhwc, drop_scales=None, taps=None):
+def forward(P, x_nhwc, drop_scales=None, taps=None, training=True, bn_stats=None):
     """ff_effnet forward. P: dict of fp64 tensors (Keras names/layouts). x_nhwc: [N,H,W,3] in
     [0,1]. drop_scales: {block_name: [N] keep/(1-rate) factors} (None = drop-connect off).
-    taps: optional dict receiving intermediate NHWC activations. Returns [N,H,W,1]."""
+    taps: optional dict receiving intermediate NHWC activations. training=False: every BN on
+    its moving statistics (Keras predict / validation; drop-connect is then off). bn_stats:
+    optional dict receiving every training-mode BN's batch mean and variance. Returns
+    [N,H,W,1]."""
+    if bn_stats is not None:
+        _STATS[0] = bn_stats
+        try:
+            return forward(P, x_nhwc, drop_scales, taps, training)
+        finally:
+            _STATS[0] = None
+    if not training:
+        _TRAINING[0] = False
+        try:
+            return forward(P, x_nhwc, None, taps, True)
+        finally:
+            _TRAINING[0] = True
     acts = taps if taps is not None else {}
     x = x_nhwc.permute(0, 3, 1, 2)
     mean = P["normalization/mean"].view(1, 3, 1, 1)

@@ -124,24 +124,8 @@ def test_inference_mode_uses_moving_statistics(step_results, cuda):
     # reference: the oracle graph with every BN in inference mode (moving statistics)
     P = {k: torch.tensor(v, dtype=torch.float64) for k, v in w.items()}
     x64 = eng.act["input"].double().cpu()
-    import oracle.effnet as oe_mod
-
-    def forward_infer():
-        saved = oe_mod._bn
-
-        def _bn(PP, name, x):
-            mm = PP[name + "/moving_mean"].view(1, -1, 1, 1)
-            mv = PP[name + "/moving_variance"].view(1, -1, 1, 1)
-            return ((x - mm) / torch.sqrt(mv + OE.BN_EPS) * PP[name + "/gamma"].view(1, -1, 1, 1)
-                    + PP[name + "/beta"].view(1, -1, 1, 1))
-        oe_mod._bn = _bn
-        try:
-            return OE.forward(P, x64)
-        finally:
-            oe_mod._bn = saved
-
     with torch.no_grad():
-        ref = forward_infer()
+        ref = OE.forward(P, x64, training=False)
     assert rel(pred, ref) < TOL
 
 
