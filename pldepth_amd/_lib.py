@@ -8,7 +8,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpldepth_hip.so")
+# PLD_LIB_PATH: load another build of the same ABI (A/B experiments, tools/ab_lib.sh)
+LIB_PATH = os.environ.get("PLD_LIB_PATH") or os.path.join(_HERE, "libpldepth_hip.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "pldepth_hip.h")
 
 P = C.c_void_p
