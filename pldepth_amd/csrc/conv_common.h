@@ -37,6 +37,11 @@ struct GemmConvParams {
   // and consecutive steps re-read the same channels at shifted taps (L2 hits)
   int kc_tap, kc1;
   FastDiv dTaps;
+  // BatchNorm batch statistics of the stored output (FWD, unsplit, overwrite, no routing):
+  // fp64 (sum, sum of squares) per output channel and per wave row tile, channel-major
+  // [N][stats_parts][2], stats_parts = M tiles x (BM / wave rows); NULL = off
+  double* stats;
+  int stats_parts;
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -92,6 +97,32 @@ __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx1
         }
       }
     return;
+  }
+  if (p.stats) {
+    // per column: this wave's rows summed in fp64 (the lane's 16 x TM rows, then the other half
+    // wave's through a cross-half swap); lanes 0-31 own one column each. Written for every wave
+    // row tile (zeros past M), so the finalize reads stats_parts whole slots per channel.
+    const int part = m_w / (TM * 32);
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n_w + b * 32 + l32;
+      const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+      double s = 0.0, q = 0.0;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const double v = row < p.M ? (double)(acc[a][b][r] + bias) : 0.0;
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 32);
+      if (h == 0 && col < p.N)
+        *reinterpret_cast<double2*>(p.stats + ((long)col * p.stats_parts + part) * 2) =
+            make_double2(s, q);
+    }
   }
 #pragma unroll
   for (int a = 0; a < TM; ++a)

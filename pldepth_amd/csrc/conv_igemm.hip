@@ -897,6 +897,22 @@ static long fwd_span_bytes(const GemmConvParams& p, int bm) {
   return imgs * p.h * p.w * (long)std::max(p.c1, p.c2) * 4;
 }
 
+// pld_conv2d_fwd_bn_stats -> run_fwd_gemm: where the forward GEMM runs unsplit on a tile
+// kernel (bf16x3 im2col or exact fp32), its epilogue writes the BN statistics partials into
+// `buf` and `parts` reports their count (0: not fused, the caller takes the separate pass)
+struct FwdStatsReq {
+  double* buf = nullptr;
+  int parts = 0;
+};
+static thread_local FwdStatsReq g_fwd_stats;
+
+static void fwd_stats_attach(GemmConvParams& p, int bm, int tm) {
+  if (!g_fwd_stats.buf || p.acc1 || p.split < p.N) return;
+  p.stats = g_fwd_stats.buf;
+  p.stats_parts = (int)cdiv(p.M, bm) * (bm / (32 * tm));
+  g_fwd_stats.parts = p.stats_parts;
+}
+
 static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void* ws,
                         size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
@@ -941,6 +957,9 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
     if (splits == 1) {
       p.ktiles_per_split = 0;
       p.zstride = 0;
+      int bm, bn, tm, tn, occ;
+      pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+      fwd_stats_attach(p, bm, tm);
       return launch(p, 1);
     }
   } else {
@@ -950,6 +969,10 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   if (splits == 1) {
     p.ktiles_per_split = 0;
     p.zstride = 0;
+    // rows per wave of the exact-fp32 tiles (launch_igemm's WM: BM / WM = 64 for cfg 1,
+    // which kTiles' cost-model tm does not state)
+    static const int kWaveRows[kNumCfg] = {64, 64, 32, 64, 32, 32, 32, 64, 128};
+    fwd_stats_attach(p, kTiles[cfg].bm, kWaveRows[cfg] / 32);
     return launch_igemm<MODE_FWD>(p, vec, vec16, 1, cfg, st);
   }
   }
@@ -1089,7 +1112,10 @@ extern "C" size_t pld_conv2d_fwd_bn_stats_workspace_size(const pld_conv_args* a)
                           ? sizeof(double) * 2 * (size_t)a->cout *
                                 pld__wide_stats_parts(rows, a->c1, a->cout)
                           : 0;
-  return std::max(std::max(thin, wide), pld_channel_reduce_workspace_size(rows, a->cout));
+  // GEMM epilogue partials: cdiv(M, BM) x BM / (32 TM) <= M / 32 + 8 per channel
+  const size_t gemm = sizeof(double) * 2 * (size_t)a->cout * (cdiv(rows, 32) + 8);
+  return std::max(std::max(std::max(thin, wide), gemm),
+                  pld_channel_reduce_workspace_size(rows, a->cout));
 }
 
 extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_ohwi,
@@ -1119,8 +1145,14 @@ extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_oh
                                 rows, a->cout, eps, momentum, mean, invstd, moving_mean,
                                 moving_var, as_stream(stream));
   }
+  g_fwd_stats = FwdStatsReq{(double*)ws, 0};
   int rc = pld_conv2d_fwd(a, w_ohwi, bias, y, 0, stream);
+  const int parts = g_fwd_stats.parts;
+  g_fwd_stats = FwdStatsReq{};
   if (rc) return rc;
+  if (parts > 0)  // gathered by the GEMM epilogue
+    return pld__bn_stats_finish((const double*)ws, parts, rows, a->cout, eps, momentum, mean,
+                                invstd, moving_mean, moving_var, as_stream(stream));
   return pld_bn_stats(y, rows, a->cout, eps, momentum, mean, invstd, moving_mean, moving_var, ws,
                       stream);
 }

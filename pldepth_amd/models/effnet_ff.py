@@ -348,18 +348,16 @@ class EffNetFF:
             x = self._block_fwd(blk, x, training, step, li)
         h, w = x.shape[1], x.shape[2]
         rows = B * h * w
-        K.conv2d_fwd(a(x, None, 1, 1, 1, 0, 0, h, w, 1280, math=self._em(h, w)), self.top.w_nat,
-                     None, A["top_pre"])
-        self.top_bn.stats_(A["top_pre"], rows, training)
+        self.top_bn.conv_fwd_stats(a(x, None, 1, 1, 1, 0, 0, h, w, 1280, math=self._em(h, w)),
+                                   self.top.w_nat, None, A["top_pre"], rows, training)
         self.top_bn.apply(A["top_pre"], rows, "swish", A["top_activation"], training)
         x, x2 = A["top_activation"], None
         for i, (conv, bn, skip) in enumerate(self.dec):
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
             args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
-            K.conv2d_fwd(args, conv.w_nat, conv.b, A[f"dec{i}_pre"])
             rows = B * h * w
-            bn.stats_(A[f"dec{i}_pre"], rows, training)
+            bn.conv_fwd_stats(args, conv.w_nat, conv.b, A[f"dec{i}_pre"], rows, training)
             if training and i == len(self.dec) - 1 and self.fuse_final:
                 pass  # BN + ReLU + upsample folded into the final conv (upconv_fwd below)
             elif training:
@@ -423,7 +421,8 @@ class EffNetFF:
         F = self.frozen
         se_w = (F[blk["se_w1"]].view(blk["cexp"], blk["cse"]), F[blk["se_b1"]],
                 F[blk["se_w2"]].view(blk["cse"], blk["cexp"]), F[blk["se_b2"]])
-        if training and blk["fused_project"]:
+        pg = training and blk["fused_project"]
+        if pg:
             # the SE squeeze applies BN + swish to dw_pre on the fly, and the project conv reads
             # dw_pre through BN + swish + the SE gate (pgemm): neither the block's activation
             # nor se_excite is materialised
@@ -444,11 +443,13 @@ class EffNetFF:
                 bn.apply(A[n + "dw_pre"], rows, "swish", A[n + "activation"], training)
                 K.se_fwd(A[n + "activation"], *se_w, blk["pooled"], blk["z1"], blk["gate"])
                 self._gate_mul(A[n + "activation"], blk["gate"], A[n + "se_excite"])
-            K.conv2d_fwd(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow,
-                                     blk["cout"], math=self._em(oh, ow)),
-                         blk["project"].w_nat, None, A[n + "project_pre"])
         pbn = blk["project_bn"]
-        pbn.stats_(A[n + "project_pre"], rows, training)
+        if pg:
+            pbn.stats_(A[n + "project_pre"], rows, training)
+        else:
+            pbn.conv_fwd_stats(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow,
+                                           blk["cout"], math=self._em(oh, ow)),
+                               blk["project"].w_nat, None, A[n + "project_pre"], rows, training)
         out = A[n + "output"]
         pbn.apply(A[n + "project_pre"], rows, "none", out, training)
         if blk["residual"]:

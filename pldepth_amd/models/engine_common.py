@@ -80,6 +80,16 @@ class _BN:
             K.bn_inference_coeffs(self.gamma, self.beta, self.mmean, self.mvar, self.inf_scale,
                                   self.inf_shift, self.eps)
 
+    def conv_fwd_stats(self, args, w_nat, bias, y, rows, training):
+        """conv forward into y, then this BN's statistics of y: in training they come from the
+        conv kernel's epilogue where it supports it (pld_conv2d_fwd_bn_stats)."""
+        if training:
+            K.conv2d_fwd_bn_stats(args, w_nat, bias, y, self.mean, self.invstd, self.mmean,
+                                  self.mvar, self.eps, self.momentum)
+        else:
+            K.conv2d_fwd(args, w_nat, bias, y)
+            self.stats_(y, rows, False)
+
     def apply(self, x, rows, act, y, training, gate=None, hw=0):
         if training:
             K.bn_apply(x, rows, self.c, self.mean, self.invstd, self.gamma, self.beta, act, y,

@@ -238,8 +238,9 @@ class RedWebFF:
         return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
                               getattr(self, "x3_min_population", None))
 
-    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None):
-        """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout]."""
+    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None, bn=None, training=True):
+        """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout];
+        with `bn`, also that BN's statistics of y (fused into the conv epilogue in training)."""
         k, s = conv.k, conv.stride
         if s == 1:
             pt, pl = (k - 1) // 2, (k - 1) // 2
@@ -247,7 +248,11 @@ class RedWebFF:
             pt = pl = 0
         args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
                            math=self._math(conv, oh, ow))
-        K.conv2d_fwd(args, conv.w_nat, conv.b, y, accumulate=acc)
+        if bn is not None:
+            assert not acc and x2 is None
+            bn.conv_fwd_stats(args, conv.w_nat, conv.b, y, self.B * oh * ow, training)
+        else:
+            K.conv2d_fwd(args, conv.w_nat, conv.b, y, accumulate=acc)
         return args
 
     def forward(self, training=True, step=0, image_offset=0):
@@ -258,8 +263,8 @@ class RedWebFF:
         args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64,
                            math=K.encoder_math(self.enc_math, B * h * w,
                                                getattr(self, "x3_min_population", None)))
-        K.conv2d_fwd(args, self.stem.w_nat, self.stem.b, A["conv1_pre"])
-        self.stem_bn.stats_(A["conv1_pre"], B * h * w, training)
+        self.stem_bn.conv_fwd_stats(args, self.stem.w_nat, self.stem.b, A["conv1_pre"], B * h * w,
+                                    training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
         K.maxpool2d_fwd(A["conv1_relu"], 3, 2, 1, 1, A["pool1_pool"], self.pool_argmax)
         x = A["pool1_pool"]
@@ -272,8 +277,7 @@ class RedWebFF:
             up = self._ffl_fwd(d, A[d["tap"]], up, training)
         h, w = up.shape[1], up.shape[2]
         rows = B * h * w
-        self._conv(self.aol0, up, A["aol/pre0"], h, w, h, w)
-        self.aol_bn.stats_(A["aol/pre0"], rows, training)
+        self._conv(self.aol0, up, A["aol/pre0"], h, w, h, w, bn=self.aol_bn, training=training)
         self.aol_bn.apply(A["aol/pre0"], rows, "relu", A["aol/act0"], training)
         self._conv(self.aol1, A["aol/act0"], A["aol/pre1"], h, w, h, w)
         K.upsample2x_fwd(A["aol/pre1"], A["aol/up"])
@@ -285,20 +289,19 @@ class RedWebFF:
         h, w, oh, ow = blk["hw"]
         rows = B * oh * ow
         if blk["proj"]:
-            self._conv(blk["c0"], x, A[n + "0_pre"], h, w, oh, ow)
-            blk["bn0"].stats_(A[n + "0_pre"], rows, training)
+            self._conv(blk["c0"], x, A[n + "0_pre"], h, w, oh, ow,
+                       bn=blk["bn0"], training=training)
             blk["bn0"].apply(A[n + "0_pre"], rows, "none", A[n + "0_bn"], training)
             sc = A[n + "0_bn"]
         else:
             sc = x
-        self._conv(blk["c1"], x, A[n + "1_pre"], h, w, oh, ow)
-        blk["bn1"].stats_(A[n + "1_pre"], rows, training)
+        self._conv(blk["c1"], x, A[n + "1_pre"], h, w, oh, ow, bn=blk["bn1"], training=training)
         blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
-        self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow)
-        blk["bn2"].stats_(A[n + "2_pre"], rows, training)
+        self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
+                   bn=blk["bn2"], training=training)
         blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
-        self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow)
-        blk["bn3"].stats_(A[n + "3_pre"], rows, training)
+        self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
+                   bn=blk["bn3"], training=training)
         blk["bn3"].add_apply(A[n + "3_pre"], rows, sc, "relu", A[n + "out"], training)
         return A[n + "out"]
 
@@ -307,15 +310,14 @@ class RedWebFF:
         rows = self.B * h * w
         for half in (0, 3):
             c, b = bt["convs"], bt["bns"]
-            self._conv(c[half], x, A[f"{n}/pre{half}"], h, w, h, w)
-            b[half].stats_(A[f"{n}/pre{half}"], rows, training)
+            self._conv(c[half], x, A[f"{n}/pre{half}"], h, w, h, w, bn=b[half], training=training)
             b[half].apply(A[f"{n}/pre{half}"], rows, "relu", A[f"{n}/act{half}"], training)
-            self._conv(c[half + 1], A[f"{n}/act{half}"], A[f"{n}/pre{half + 1}"], h, w, h, w)
-            b[half + 1].stats_(A[f"{n}/pre{half + 1}"], rows, training)
+            self._conv(c[half + 1], A[f"{n}/act{half}"], A[f"{n}/pre{half + 1}"], h, w, h, w,
+                       bn=b[half + 1], training=training)
             b[half + 1].apply(A[f"{n}/pre{half + 1}"], rows, "relu", A[f"{n}/act{half + 1}"],
                               training)
-            self._conv(c[half + 2], A[f"{n}/act{half + 1}"], A[f"{n}/pre{half + 2}"], h, w, h, w)
-            b[half + 2].stats_(A[f"{n}/pre{half + 2}"], rows, training)
+            self._conv(c[half + 2], A[f"{n}/act{half + 1}"], A[f"{n}/pre{half + 2}"], h, w, h, w,
+                       bn=b[half + 2], training=training)
             b[half + 2].add_apply(A[f"{n}/pre{half + 2}"], rows, x, "relu", A[f"{n}/out{half}"],
                                   training)
             x = A[f"{n}/out{half}"]
@@ -325,12 +327,11 @@ class RedWebFF:
         A, n = self.act, d["name"]
         h, w = d["hw"]
         rows = self.B * h * w
-        self._conv(d["conv0"], left, A[n + "/left_pre"], h, w, h, w)
-        d["bn0"].stats_(A[n + "/left_pre"], rows, training)
+        self._conv(d["conv0"], left, A[n + "/left_pre"], h, w, h, w,
+                   bn=d["bn0"], training=training)
         d["bn0"].apply(A[n + "/left_pre"], rows, "none", A[n + "/left_bn"], training)
         xl = self._bottleneck_fwd(d["left"], A[n + "/left_bn"], h, w, training)
-        self._conv(d["conv1"], up, A[n + "/up_pre"], h, w, h, w)
-        d["bn1"].stats_(A[n + "/up_pre"], rows, training)
+        self._conv(d["conv1"], up, A[n + "/up_pre"], h, w, h, w, bn=d["bn1"], training=training)
         d["bn1"].add_apply(A[n + "/up_pre"], rows, xl, "none", A[n + "/sum"], training)
         xd = self._bottleneck_fwd(d["down"], A[n + "/sum"], h, w, training)
         K.upsample2x_fwd(xd, A[n + "/out"])

@@ -952,6 +952,45 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
 
 
+@pytest.mark.parametrize("math", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("n,h,w,cin,c2,k,cout", [(2, 13, 11, 48, 16, 3, 72),
+                                                (1, 23, 29, 64, 0, 1, 200),
+                                                (3, 9, 10, 96, 0, 3, 40)])
+def test_conv_fwd_bn_stats_gemm_epilogue(cuda, math, n, h, w, cin, c2, k, cout):
+    """BN statistics from the im2col GEMM epilogue (conv_x3_kernel / conv_igemm_kernel, unsplit
+    schedules; split-K schedules take the separate pass) on every schedule: same output, same
+    statistics as pld_conv2d_fwd + pld_bn_stats on that schedule. Ragged M tiles (rows % BM),
+    ragged N tiles, a concat input and a bias (the statistics are of the stored y)."""
+    g = torch.Generator(device=cuda).manual_seed(cin * cout + h + k)
+    x = torch.randn(n, h, w, cin, device=cuda, generator=g)
+    x2 = torch.randn(n, h, w, c2, device=cuda, generator=g) if c2 else None
+    wt = torch.randn(k, k, cin + c2, cout, device=cuda, generator=g) / (k * k * cin) ** 0.5
+    b = torch.randn(cout, device=cuda, generator=g) + 0.5
+    wn = K.filter_to_native(wt)
+    rows = n * h * w
+    p = (k - 1) // 2
+    n_sched = _lib.lib().pld_conv_num_schedules(K.MATH[math])
+    fused = 0
+    for t in range(n_sched):
+        args = K.conv_args(x, x2, k, k, 1, p, p, h, w, cout, math=math)
+        args.tile = t
+        y_ref = torch.empty(n, h, w, cout, device=cuda)
+        K.conv2d_fwd(args, wn, b, y_ref)
+        m_ref, i_ref = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+        mm_ref, mv_ref = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+        K.bn_stats(y_ref, rows, cout, m_ref, i_ref, mm_ref, mv_ref)
+        y = torch.empty_like(y_ref)
+        m, i = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+        mm, mv = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+        K.conv2d_fwd_bn_stats(args, wn, b, y, m, i, mm, mv)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y_ref), t
+        for a, r in ((m, m_ref), (i, i_ref), (mm, mm_ref), (mv, mv_ref)):
+            assert rel_err(a, r) < 1e-6, (t, rel_err(a, r))
+        fused += _lib.lib().pld_conv_schedule_class(K.MATH[math], t) in (0, 3)
+    assert fused > 0
+
+
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 20, 17, 40, 240), (1, 13, 11, 112, 672),
                                             (3, 7, 9, 80, 480), (1, 6, 5, 8, 520),
                                             (2, 9, 9, 128, 1152), (1, 3, 7, 56, 200)])
