@@ -531,6 +531,44 @@ __global__ __launch_bounds__(256) void stride_scatter_kernel(const float* __rest
   }
 }
 
+// The same with 4 channels per thread and 32-bit magic-number division (C, c1 % 4 == 0,
+// 16-byte aligned buffers, < 2^31 elements): one (pixel, channel quad) per trip, the quad read
+// only at the stride grid's pixels — the generic form's three 64-bit div/mod per element bound
+// it by the ALU at ~2.4 TB/s
+__global__ __launch_bounds__(256) void stride_scatter4_kernel(const float* __restrict__ t,
+                                                              int total4, FastDiv dC4,
+                                                              FastDiv dW, FastDiv dH, int oh,
+                                                              int ow, int sh, int sw, int C,
+                                                              float* out1, int c1, int acc1,
+                                                              float* out2, int acc2) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = dC4.div((uint32_t)i);
+    const int c = 4 * (i - (int)pix * (int)dC4.d);
+    const uint32_t r = dW.div(pix);
+    const int x = (int)(pix - r * dW.d);
+    const uint32_t img = dH.div(r);
+    const int y = (int)(r - img * dH.d);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ys = y / sh, xs = x / sw;
+    if (y - ys * sh == 0 && x - xs * sw == 0 && ys < oh && xs < ow)
+      v = *reinterpret_cast<const float4*>(t + (((long)img * oh + ys) * ow + xs) * C + c);
+    float4* d;
+    int acc;
+    if (c < c1) {
+      d = reinterpret_cast<float4*>(out1 + (long)pix * c1 + c);
+      acc = acc1;
+    } else {
+      d = reinterpret_cast<float4*>(out2 + (long)pix * (C - c1) + (c - c1));
+      acc = acc2;
+    }
+    if (acc) {
+      const float4 o = *d;
+      v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    }
+    *d = v;
+  }
+}
+
 // HWIO [kh][kw][ci][co] -> [co][kh][kw][ci]
 __global__ void filter_native_kernel(const float* __restrict__ w, int taps, int cin, int cout,
                                      float* __restrict__ o) {
@@ -737,7 +775,13 @@ static int fill_geom(const pld_conv_args* a, GemmConvParams& p) {
 
 using namespace pld;
 
-// direct kernels for the single-output-channel 3x3 conv (skinny.hip)
+// direct kernels for the single-output-channel 3x3 conv and the 1 -> 1 channel 1x1 (skinny.hip)
+extern "C" int pld__scalar1x1_eligible(const pld_conv_args* a);
+extern "C" int pld__scalar1x1_apply(const float* x, const float* w, const float* bias, float* y,
+                                    long n, int accumulate, void* stream);
+extern "C" size_t pld__scalar1x1_wgrad_ws(void);
+extern "C" int pld__scalar1x1_wgrad(const float* x, const float* dy, float* dw, long n,
+                                    int accumulate, void* ws, void* stream);
 extern "C" int pld__skinny_eligible(const pld_conv_args* a);
 extern "C" int pld__skinny_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,
                                float* y, int accumulate, void* stream);
@@ -1065,6 +1109,9 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   int rc = fill_geom(a, p);
   if (rc) return rc;
   PLD_CHECK_ARG(w_ohwi && y, "pld_conv2d_fwd: null w/y");
+  if (pld__scalar1x1_eligible(a) && aligned16(a->x1) && aligned16(y))
+    return pld__scalar1x1_apply(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, accumulate,
+                                stream);
   if (pld__skinny_eligible(a) && aligned16(a->x1))
     return pld__skinny_fwd(a, w_ohwi, bias, y, accumulate, stream);
   if (pld__thin_geom(a) && pld__thin_ok(a->c1, a->cout) && aligned16(a->x1) && aligned16(y) &&
@@ -1177,6 +1224,7 @@ extern "C" int pld_conv_schedule_class(int math, int idx) {
 
 extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
   if (!a || mode < 0 || mode > 2) return -1;
+  if (pld__scalar1x1_eligible(a)) return PLD_KIND_DIRECT;
   if (pld__skinny_eligible(a) && !(mode == 1 && (a->sh != 1 || a->sw != 1)))
     return PLD_KIND_DIRECT;
   if (mode != 2 && pld__thin_geom(a) &&
@@ -1204,6 +1252,8 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
   const int kind = pld_conv_kernel_kind(a, mode);
   if (kind < 0) return "";
   if (kind == PLD_KIND_DIRECT) {
+    if (pld__scalar1x1_eligible(a))
+      return mode == 2 ? "scalar1x1_wgrad_kernel" : "scalar1x1_kernel";
     if (pld__skinny_eligible(a))
       return mode == 0 ? "skinny_fwd_kernel" : mode == 1 ? "skinny_dgrad_kernel"
                                                          : "skinny_wgrad_kernel";
@@ -1232,7 +1282,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
 
 extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
-  if (pld__skinny_eligible(a)) return 0;
+  if (pld__skinny_eligible(a) || pld__scalar1x1_eligible(a)) return 0;
   return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
                       (long)a->kh * a->kw * (a->c1 + a->c2), a->kh * a->kw, a->c1, a->c2, a->tile,
                       a->math,
@@ -1246,7 +1296,7 @@ static size_t strided_tmp_bytes(const pld_conv_args* a) {
 
 extern "C" size_t pld_conv2d_dgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->h <= 0 || a->w <= 0) return 0;
-  if (pld__skinny_eligible(a)) return 0;
+  if (pld__skinny_eligible(a) || pld__scalar1x1_eligible(a)) return 0;
   const bool geom = x3_fwd_geom(a->cout, a->cout, false, a->kh * a->kw);
   const bool hs = a->w_split != nullptr;
   if (a->sh != 1 || a->sw != 1)  // 1x1 strided: GEMM into a compact tmp, then scatter
@@ -1311,11 +1361,23 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
                       "pld_conv2d_dgrad", a->math);
     if (rc) return rc;
     const long total = (long)a->n * a->h * a->w * C;
+    if (C % 4 == 0 && a->c1 % 4 == 0 && aligned16(t) && aligned16(dx1) &&
+        (!dx2 || aligned16(dx2))) {
+      const int total4 = (int)(total / 4);
+      stride_scatter4_kernel<<<std::min<unsigned>(cdiv(total4, 256), 16384), 256, 0, st>>>(
+          t, total4, FastDiv((uint32_t)(C / 4)), FastDiv((uint32_t)a->w),
+          FastDiv((uint32_t)a->h), a->oh, a->ow, a->sh, a->sw, C, dx1, a->c1, accumulate1, dx2,
+          accumulate2);
+      return check_launch("stride_scatter4_kernel");
+    }
     stride_scatter_kernel<<<std::min<unsigned>(cdiv(total, 256), 16384), 256, 0, st>>>(
         t, a->n, a->h, a->w, a->oh, a->ow, a->sh, a->sw, C, dx1, a->c1, accumulate1, dx2,
         accumulate2);
     return check_launch("stride_scatter_kernel");
   }
+  if (pld__scalar1x1_eligible(a) && aligned16(dy) && aligned16(dx1))
+    return pld__scalar1x1_apply(dy, w_dgrad, nullptr, dx1, (long)a->n * a->h * a->w,
+                                accumulate1, stream);
   if (pld__skinny_eligible(a) && aligned16(dx1))
     return pld__skinny_dgrad(a, dy, w_dgrad, dx1, accumulate1, stream);
   // 1x1: w_dgrad is [cin][cout], dx = dy . w_dgrad^T
@@ -1436,6 +1498,7 @@ extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->kh <= 0 || a->kw <= 0 || a->c1 <= 0 || a->c2 < 0 || a->cout <= 0 ||
       a->oh <= 0 || a->ow <= 0)
     return 0;
+  if (pld__scalar1x1_eligible(a)) return pld__scalar1x1_wgrad_ws();
   if (pld__skinny_eligible(a)) return pld__skinny_wgrad_ws(a);
   int M, N, splits, kt, cfg;
   long K;
@@ -1450,6 +1513,12 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   int rc = fill_geom(a, p);
   if (rc) return rc;
   PLD_CHECK_ARG(dy && dw, "pld_conv2d_wgrad: null dy/dw");
+  if (pld__scalar1x1_eligible(a) && aligned16(a->x1) && aligned16(dy)) {
+    const size_t need = pld__scalar1x1_wgrad_ws();
+    PLD_CHECK_ARG(ws && ws_bytes >= need, "pld_conv2d_wgrad: workspace %zu < %zu bytes",
+                  ws_bytes, need);
+    return pld__scalar1x1_wgrad(a->x1, dy, dw, (long)a->n * a->h * a->w, accumulate, ws, stream);
+  }
   if (pld__skinny_eligible(a) && aligned16(a->x1)) {
     const size_t need = pld__skinny_wgrad_ws(a);
     PLD_CHECK_ARG(ws && ws_bytes >= need, "pld_conv2d_wgrad: workspace %zu < %zu bytes",

@@ -277,9 +277,110 @@ __global__ __launch_bounds__(256) void skinny_wgrad_reduce_kernel(const float* _
 constexpr int SKINNY_WG_BLOCKS = 2048;
 constexpr int SKINNY_FWD_BLOCKS = 2048;  // persistent: ~3 per CU, each over a strided tile set
 
+// ---- 1x1 conv with one input and one output channel (ReDWeb's final aol/conv2, redweb.py: a
+// scalar affine map of the 448^2 prediction): y = w x + b, dx = w dy, dw = sum x dy. Pure HBM
+// streams — as an implicit GEMM with K = N = 1 it ran at 0.4 ms fwd / dgrad and 1.3 ms wgrad.
+constexpr int SCALAR_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void scalar1x1_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ y, long n, int acc) {
+  const float wv = w[0], bv = bias ? bias[0] : 0.f;
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    float4 o = make_float4(wv * v.x + bv, wv * v.y + bv, wv * v.z + bv, wv * v.w + bv);
+    if (acc) {
+      const float4 d = reinterpret_cast<const float4*>(y)[i];
+      o = make_float4(d.x + o.x, d.y + o.y, d.z + o.z, d.w + o.w);
+    }
+    reinterpret_cast<float4*>(y)[i] = o;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long i = 4 * n4 + threadIdx.x;
+    const float o = wv * x[i] + bv;
+    y[i] = acc ? y[i] + o : o;
+  }
+}
+
+// fp64 partial dot products, one per block (fixed grid-stride order), then one ordered sum
+__global__ __launch_bounds__(256) void scalar1x1_wgrad_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ dy,
+                                                              long n, double* __restrict__ part) {
+  __shared__ double red[4];
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(x)[i];
+    const float4 b = reinterpret_cast<const float4*>(dy)[i];
+    s += (double)a.x * b.x + (double)a.y * b.y + (double)a.z * b.z + (double)a.w * b.w;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long i = 4 * n4 + threadIdx.x;
+    s += (double)x[i] * dy[i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void scalar1x1_wgrad_sum_kernel(const double* __restrict__ part,
+                                                                  int nb, float* __restrict__ dw,
+                                                                  int acc) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = (float)((red[0] + red[1]) + (red[2] + red[3]));
+    dw[0] = acc ? dw[0] + v : v;
+  }
+}
+
 }  // namespace pld
 
 using namespace pld;
+
+extern "C" int pld__scalar1x1_eligible(const pld_conv_args* a) {
+  return a && a->kh == 1 && a->kw == 1 && a->sh == 1 && a->sw == 1 && a->pad_t == 0 &&
+         a->pad_l == 0 && a->c1 == 1 && a->c2 == 0 && a->cout == 1 && a->in_scale == nullptr &&
+         a->oh == a->h && a->ow == a->w;
+}
+
+static unsigned scalar_grid(long n) {
+  return (unsigned)std::max<long>(1, std::min<long>(SCALAR_BLOCKS, ((n >> 2) + 255) / 256));
+}
+
+// fwd: (x, w, b) -> y; dgrad: (dy, w, NULL) -> dx (the 1x1 1->1 filter is its own transpose)
+extern "C" int pld__scalar1x1_apply(const float* x, const float* w, const float* bias, float* y,
+                                    long n, int accumulate, void* stream) {
+  PLD_CHECK_ARG(x && w && y && aligned16(x) && aligned16(y), "scalar 1x1 conv: bad args");
+  scalar1x1_kernel<<<scalar_grid(n), 256, 0, as_stream(stream)>>>(x, w, bias, y, n, accumulate);
+  return check_launch("scalar1x1_kernel");
+}
+
+extern "C" size_t pld__scalar1x1_wgrad_ws(void) { return sizeof(double) * SCALAR_BLOCKS; }
+
+extern "C" int pld__scalar1x1_wgrad(const float* x, const float* dy, float* dw, long n,
+                                    int accumulate, void* ws, void* stream) {
+  PLD_CHECK_ARG(x && dy && dw && ws && aligned16(x) && aligned16(dy),
+                "scalar 1x1 wgrad: bad args");
+  const unsigned nb = scalar_grid(n);
+  hipStream_t st = as_stream(stream);
+  scalar1x1_wgrad_kernel<<<nb, 256, 0, st>>>(x, dy, n, (double*)ws);
+  int rc = check_launch("scalar1x1_wgrad_kernel");
+  if (rc) return rc;
+  scalar1x1_wgrad_sum_kernel<<<1, 256, 0, st>>>((const double*)ws, (int)nb, dw, accumulate);
+  return check_launch("scalar1x1_wgrad_sum_kernel");
+}
 
 // eligibility: 3x3 stride-1 'same', single source, no prologue, cout 1, c % 4 == 0, c <= 64
 extern "C" int pld__skinny_eligible(const pld_conv_args* a) {

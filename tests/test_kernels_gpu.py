@@ -106,6 +106,8 @@ CONV_CASES = [
     (1, 9, 9, 32, 64, 3, 1, 240, True, False),     # N=240; dgrad splits 32|64
     (1, 8, 8, 96, 0, 3, 1, 224, True, False),      # N=224 exact tile
     (3, 5, 7, 320, 0, 1, 1, 1280, False, False),   # top conv shape class
+    (2, 37, 45, 1, 0, 1, 1, 1, True, False),       # 1 -> 1 channel 1x1 (ReDWeb aol/conv2):
+    (4, 64, 64, 1, 0, 1, 1, 1, True, False),       #   scalar kernels, ragged and float4 tails
 ]
 
 
@@ -175,6 +177,32 @@ def test_conv_fwd_dgrad_wgrad(cuda, case, math):
         assert rel_err(dx1, x1r.grad) < tol, rel_err(dx1, x1r.grad)
         if x2 is not None:
             assert rel_err(dx2 - 1.0, x2r.grad) < tol
+
+
+@pytest.mark.parametrize("math", MATHS)
+@pytest.mark.parametrize("n,h,w,c,cout", [(2, 14, 12, 64, 128), (1, 9, 11, 32, 48),
+                                          (2, 7, 7, 6, 8)])
+def test_conv_dgrad_strided_1x1(cuda, math, n, h, w, c, cout):
+    """dgrad of a stride-2 1x1 conv (ResNet projection shortcuts / first 1x1 of a stage): the
+    GEMM on the output grid, then the scatter into the input grid (zeros off the stride grid),
+    overwrite and accumulate; odd input sizes; C % 4 != 0 takes the generic scatter."""
+    torch.manual_seed(n * h + c)
+    x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
+    wt = torch.randn(1, 1, c, cout, dtype=torch.float64) / np.sqrt(c)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = OE.conv(x.permute(0, 3, 1, 2), wt, None, 2, (0, 0, 0, 0)).permute(0, 2, 3, 1)
+    assert y.shape[1:3] == (oh, ow)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    gx = dev(x.detach(), cuda)
+    args = K.conv_args(gx, None, 1, 1, 2, 0, 0, oh, ow, cout, math=math)
+    dx = torch.full_like(gx, 0.25)
+    K.conv2d_dgrad(args, dev(dy, cuda), K.filter_to_dgrad(dev(wt, cuda)), dx, acc1=True)
+    torch.cuda.synchronize()
+    assert rel_err(dx - 0.25, x.grad) < CONV_TOL[math]
+    K.conv2d_dgrad(args, dev(dy, cuda), K.filter_to_dgrad(dev(wt, cuda)), dx)
+    torch.cuda.synchronize()
+    assert rel_err(dx, x.grad) < CONV_TOL[math]
 
 
 @pytest.mark.parametrize("math", MATHS)
