@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tile", type=int, default=-1, help="-1 = autotune")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--presplit", type=int, default=1)
+    ap.add_argument("--acc", type=int, default=0, help="accumulate into the destination")
     a = ap.parse_args()
     from pldepth_amd import kernels as K
     torch.cuda.set_device(0)
@@ -51,8 +52,8 @@ def main():
     dy = torch.randn_like(y)
     dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if x2 is not None else None)
     dw = torch.empty_like(w)
-    run = {"fwd": lambda: K.conv2d_fwd(args, wn, None, y),
-           "dgrad": lambda: K.conv2d_dgrad(args, dy, wd, dx1, dx2),
+    run = {"fwd": lambda: K.conv2d_fwd(args, wn, None, y, accumulate=bool(a.acc)),
+           "dgrad": lambda: K.conv2d_dgrad(args, dy, wd, dx1, dx2, acc1=bool(a.acc)),
            "wgrad": lambda: K.conv2d_wgrad(args, dy, dw)}[a.mode]
     run()
     torch.cuda.synchronize()
