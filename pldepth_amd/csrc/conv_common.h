@@ -124,6 +124,29 @@ __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx1
             make_double2(s, q);
     }
   }
+  if (!p.acc1 && !p.acc2) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n_w + b * 32 + l32;
+        if (col >= p.N) continue;
+        const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row >= p.M) continue;
+          const float v = acc[a][b][r] + bias;
+          if (col < p.split) p.out1[(long)row * p.ld1 + col] = v;
+          else p.out2[(long)row * p.ld2 + (col - p.split)] = v;
+        }
+      }
+    return;
+  }
+  // accumulate: the tile's 16 destination values are fetched together before any store (one
+  // HBM latency per tile instead of one per element: the compiler cannot prove the
+  // read-modify-writes independent, so it would not batch them itself; 0.80 -> 0.55 ms on a
+  // 401408 x 512 -> 256 dgrad)
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -131,18 +154,22 @@ __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx1
       const int col = n_w + b * 32 + l32;
       if (col >= p.N) continue;
       const float bias = p.bias ? p.bias[col] : 0.f;
+      const bool first = col < p.split;  // two-way column routing (dgrad of a concat)
+      float* base = first ? p.out1 + col : p.out2 + (col - p.split);
+      const long ld = first ? p.ld1 : p.ld2;
+      const int accum = first ? p.acc1 : p.acc2;
+      float prev[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        prev[r] = (accum && row < p.M) ? base[(long)row * ld] : 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
         const float v = acc[a][b][r] + bias;
-        if (col < p.split) {
-          float* dst = p.out1 + (long)row * p.ld1 + col;
-          *dst = p.acc1 ? *dst + v : v;
-        } else {
-          float* dst = p.out2 + (long)row * p.ld2 + (col - p.split);
-          *dst = p.acc2 ? *dst + v : v;
-        }
+        base[(long)row * ld] = accum ? prev[r] + v : v;
       }
     }
 }
