@@ -763,6 +763,10 @@ def test_maxpool_zero_padded(cuda, shape, relu):
     torch.cuda.synchronize()
     assert rel_err(y, y_ref) == 0.0
     assert rel_err(dx, xr.grad) < 1e-6
+    dx.fill_(0.5)
+    K.maxpool2d_bwd(dev(dy, cuda), am, 3, 2, 1, 1, dx, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(dx - 0.5, xr.grad) < 1e-6
 
 
 @pytest.mark.parametrize("rows,c,act", [(3000, 64, "relu"), (517, 256, "none"),
