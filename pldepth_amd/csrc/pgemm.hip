@@ -146,11 +146,31 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgParams p) {
   __builtin_amdgcn_wave_barrier();
   const int ncol = min(NW, p.N - nb);
   if (ncol <= 0) return;
-  for (int e = lane; e < rows * ncol; e += 64) {
-    const int r = e / ncol, j = e - r * ncol;
-    float* d = p.y + (m0 + r) * p.N + nb + j;
-    const float v = sw[r * LO + j];
-    *d = p.acc ? *d + v : v;
+  if (!p.acc) {
+    for (int e = lane; e < rows * ncol; e += 64) {
+      const int r = e / ncol, j = e - r * ncol;
+      p.y[(m0 + r) * p.N + nb + j] = sw[r * LO + j];
+    }
+    return;
+  }
+  // accumulate: 8 destination values fetched together per trip (one HBM latency per 8
+  // read-modify-writes: the compiler will not reorder them across the possibly aliasing stores)
+  constexpr int U = 8;
+  for (int e0 = lane; e0 < rows * ncol; e0 += 64 * U) {
+    float old[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 64 * u;
+      const int r = e / ncol, j = e - r * ncol;
+      old[u] = e < rows * ncol ? p.y[(m0 + r) * p.N + nb + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 64 * u;
+      if (e >= rows * ncol) break;
+      const int r = e / ncol, j = e - r * ncol;
+      p.y[(m0 + r) * p.N + nb + j] = old[u] + sw[r * LO + j];
+    }
   }
 }
 

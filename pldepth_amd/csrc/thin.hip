@@ -92,6 +92,15 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
     }
     // rows x CH chunk: CH/4 lanes per row, 64 / (CH/4) rows per store instruction
     constexpr int QPR = CH / 4;
+    float4 old[QPR];  // accumulate: the destination quads fetched before any store
+#pragma unroll
+    for (int j = 0; j < QPR; ++j) {
+      const int e = lane + 64 * j;
+      const int r = e / QPR, q = e % QPR;
+      old[j] = (acc && r < rows)
+                   ? *reinterpret_cast<const float4*>(out + (m0 + r) * N + n0 + 4 * q)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int j = 0; j < QPR; ++j) {
       const int e = lane + 64 * j;
@@ -99,7 +108,7 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
       if (r < rows) {
         float4 v = *reinterpret_cast<const float4*>(sw + r * LO + 4 * q);
         float4* d = reinterpret_cast<float4*>(out + (m0 + r) * N + n0 + 4 * q);
-        if (acc) v = add4(v, *d);
+        if (acc) v = add4(v, old[j]);
         *d = v;
       }
     }
