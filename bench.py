@@ -139,6 +139,8 @@ def attach_traffic(roof, path, workload):
     """roofline.traffic = HBM bytes per launch of the dominant kernel from the committed PMC
     profile (tools/dominant_traffic.py), only when that profile measured the same kernel on the
     same workload; otherwise it stays null."""
+    if path and not os.path.isabs(path):  # relative to the repository, whatever the cwd
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), path)
     try:
         with open(path) as f:
             t = json.load(f)
