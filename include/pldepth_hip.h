@@ -372,6 +372,22 @@ int pld_dwconv_fwd_bn_stats(const float* x, int n, int h, int w, int c, const fl
 int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw, int k, int s,
                      int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
                      void* stream);
+/* pld_dwconv_dgrad into dact (= d act(bn(x)), the gradient at the depthwise input) fused with
+ * the backward of that BatchNormalization + activation (the MBConv expand BN,
+ * pl_hourglass.py:52-57 via Keras EfficientNetB0 block{i}expand_bn / expand_activation): its
+ * reductions (sum dz, sum dz xhat, dz = dact act'(bn(x))) are gathered as dact is stored, then
+ * dgamma / dbeta (param_accumulate) and k12 = [mean dz | mean dz xhat] (2c floats) are
+ * finalized, and, when dx != NULL, dx (= the BN input gradient, dx_accumulate) is written as
+ * pld_bn_bwd does. dx == NULL: coefficients only (for pld_pgemm_bn_bwd). x / mean / invstd /
+ * gamma / beta 16-byte aligned. Workspace: pld_dwconv_dgrad_bn_bwd_workspace_size. */
+size_t pld_dwconv_dgrad_bn_bwd_workspace_size(int n, int h, int w, int c, int s);
+int pld_dwconv_dgrad_bn_bwd(const float* dy, int n, int h, int w, int c, const float* wdw, int k,
+                            int s, int pad_t, int pad_l, int oh, int ow, float* dact,
+                            int accumulate, const float* x, const float* mean,
+                            const float* invstd, const float* gamma, const float* beta, int act,
+                            float* dx, int dx_accumulate, float* dgamma, float* dbeta,
+                            int param_accumulate, float* k12, void* ws, size_t ws_bytes,
+                            void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * EfficientNet squeeze-and-excitation (frozen FCs, gradient flows to the input):

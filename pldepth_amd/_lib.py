@@ -101,6 +101,9 @@ _SIGS = {
     "pld_dwconv_fwd_bn_stats": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P,
                                       P, P, P, I32, P, F32, F32, P, P, P, P, P, SZ, P]),
     "pld_dwconv_dgrad": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, I32, P]),
+    "pld_dwconv_dgrad_bn_bwd_workspace_size": (SZ, [I32, I32, I32, I32, I32]),
+    "pld_dwconv_dgrad_bn_bwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P,
+                                      I32, P, P, P, P, P, I32, P, I32, P, P, I32, P, P, SZ, P]),
     "pld_se_workspace_size": (SZ, [I32, I32, I32, I32]),
     "pld_se_fwd": (I32, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P]),
     "pld_se_bwd": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P]),
@@ -135,7 +138,8 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_ti
                "pld_channel_reduce_workspace_size", "pld_se_workspace_size",
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",
-               "pld_upconv_bwd_workspace_size", "pld_se_bwd_bn_full_workspace_size"}
+               "pld_upconv_bwd_workspace_size", "pld_se_bwd_bn_full_workspace_size",
+               "pld_dwconv_dgrad_bn_bwd_workspace_size"}
 
 
 def declared_symbols(header=HEADER):

@@ -121,17 +121,104 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
   }
 }
 
+// Optional epilogue of the depthwise dgrads: the backward reductions of the BN + activation
+// that PRODUCED the depthwise input (an MBConv expand BN: x = its pre-BN input), gathered as the
+// gradient d(act) is stored — dz = d(act) act'(bn(x)), per channel (sum dz, sum dz xhat) in fp64.
+// The host sizes the grid to a multiple of the channel-quad count, so each thread's quad is fixed
+// for all its trips; a block combines its threads per quad in a fixed order and writes one
+// partial per channel: [C][gridDim.x][2], bn.hip's finalize layout (no separate pass over
+// (x, d(act)) for the reductions).
+struct DwBnb {
+  const float* x;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  double* part;
+};
+
+// the BN parameters of this thread's (fixed) channel quad, loaded once per launch
+struct BnbQuad {
+  float m[4], iv[4], gv[4], bv[4];
+};
+
+__device__ __forceinline__ BnbQuad bnb_quad(const DwBnb& b, int cv) {
+  const int c0 = 4 * (int)(((long)blockIdx.x * blockDim.x + threadIdx.x) % cv);
+  const float4 mu = *reinterpret_cast<const float4*>(b.mean + c0);
+  const float4 is = *reinterpret_cast<const float4*>(b.invstd + c0);
+  const float4 ga = *reinterpret_cast<const float4*>(b.gamma + c0);
+  const float4 be = *reinterpret_cast<const float4*>(b.beta + c0);
+  return BnbQuad{{mu.x, mu.y, mu.z, mu.w}, {is.x, is.y, is.z, is.w},
+                 {ga.x, ga.y, ga.z, ga.w}, {be.x, be.y, be.z, be.w}};
+}
+
+// one stored quad: fp32 running sums of the trip (a trip's few outputs), folded into the
+// thread's fp64 totals once per trip by bnb_fold
+__device__ __forceinline__ void bnb_acc(const DwBnb& b, const BnbQuad& pq, long idx, float4 v,
+                                        float (&f0)[4], float (&f1)[4]) {
+  const float4 x = *reinterpret_cast<const float4*>(b.x + idx);
+  const float xv[4] = {x.x, x.y, x.z, x.w}, dv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float xh = (xv[u] - pq.m[u]) * pq.iv[u];
+    const float dz = dv[u] * act_grad(b.act, xh * pq.gv[u] + pq.bv[u]);
+    f0[u] += dz;
+    f1[u] = fmaf(dz, xh, f1[u]);
+  }
+}
+
+__device__ __forceinline__ void bnb_fold(float (&f0)[4], float (&f1)[4], double (&s0)[4],
+                                         double (&s1)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    s0[u] += (double)f0[u];
+    s1[u] += (double)f1[u];
+    f0[u] = f1[u] = 0.f;
+  }
+}
+
+// block combine (all 256 threads reach it): thread j's quad is (blockIdx.x 256 + j) mod cv
+__device__ __forceinline__ void bnb_flush(const DwBnb& b, int cv, const double (&s0)[4],
+                                          const double (&s1)[4]) {
+  __shared__ double red[256][8];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    red[threadIdx.x][u] = s0[u];
+    red[threadIdx.x][4 + u] = s1[u];
+  }
+  __syncthreads();
+  const int base = (int)(((long)blockIdx.x * 256) % cv);
+  for (int qq = threadIdx.x; qq < cv; qq += 256) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, c[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = (qq - base + cv) % cv; j < 256; j += cv)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += red[j][u];
+        c[u] += red[j][4 + u];
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<double2*>(b.part + ((long)(4 * qq + u) * gridDim.x + blockIdx.x) * 2) =
+          make_double2(a[u], c[u]);
+  }
+}
+
 // input gradient, stride 1: dx[iy][ix] = sum dy[iy+pt-ty][ix+pl-tx] w[ty][tx]; a thread owns
 // R rows x T columns of dx from an (R+K-1) x (T+K-1) window of dy, each dy row loaded once. dy
 // rows are visited bottom-up so every output still sums its taps in ascending (ty, tx) order.
-template <int K, int T, int R>
+template <int K, int T, int R, bool BNB = false>
 __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __restrict__ dy,
                                                               const float* __restrict__ wt,
                                                               DwGeom g, float* __restrict__ dx,
-                                                              int accum) {
+                                                              int accum, DwBnb bnb = DwBnb{}) {
   constexpr int NC = T + K - 1;
   constexpr int NR = R + K - 1;
   const int cv = g.c / 4;
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+  float f0[4] = {0.f, 0.f, 0.f, 0.f}, f1[4] = {0.f, 0.f, 0.f, 0.f};
+  BnbQuad pq{};
+  if constexpr (BNB) pq = bnb_quad(bnb, cv);
   const int tiles = (g.w + T - 1) / T;
   const int rgroups = (g.h + R - 1) / R;
   const int total = g.n * rgroups * tiles * cv;
@@ -190,9 +277,14 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __res
           v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
         }
         *d = v;
+        if constexpr (BNB)
+          bnb_acc(bnb, pq, (((long)img * g.h + iy0 + r) * g.w + ix0 + o) * g.c + 4 * q, v, f0,
+                  f1);
       }
     }
+    if constexpr (BNB) bnb_fold(f0, f1, s0, s1);
   }
+  if constexpr (BNB) bnb_flush(bnb, cv, s0, s1);
 }
 
 // input gradient, stride 2, one thread per 2x2 block of dx pixels (2a + u, 2b + v). With the pad
@@ -201,14 +293,18 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s1_kernel(const float* __res
 // outputs — and dy row (2a + u + pt - ty) / 2 = a + pt / 2 + (u + PTP - ty) / 2: a window of
 // (K + 3) / 2 dy rows x columns at compile-time offsets, each loaded once (the per-pixel kernel
 // re-read it for every output). Each output sums its taps in ascending (ty, tx) order.
-template <int K, int PTP, int PLP>
+template <int K, int PTP, int PLP, bool BNB = false>
 __global__ __launch_bounds__(256) void dwconv_dgrad_s2_kernel(const float* __restrict__ dy,
                                                               const float* __restrict__ wt,
                                                               DwGeom g, float* __restrict__ dx,
-                                                              int accum) {
+                                                              int accum, DwBnb bnb = DwBnb{}) {
   constexpr int DMIN = -(K - 1) / 2;  // (u + PTP - ty) / 2 ranges over [DMIN, 1]
   constexpr int NW = 2 - DMIN;
   const int cv = g.c / 4;
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+  float f0[4] = {0.f, 0.f, 0.f, 0.f}, f1[4] = {0.f, 0.f, 0.f, 0.f};
+  BnbQuad pq{};
+  if constexpr (BNB) pq = bnb_quad(bnb, cv);
   const int bw = (g.w + 1) / 2, bh = (g.h + 1) / 2;
   const int total = g.n * bh * bw * cv;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -256,16 +352,20 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_s2_kernel(const float* __res
       for (int v = 0; v < 2; ++v) {
         const int ix = 2 * b + v;
         if (ix >= g.w) continue;
-        float4* d = reinterpret_cast<float4*>(dx + (((long)img * g.h + iy) * g.w + ix) * g.c + 4 * q);
+        const long idx = (((long)img * g.h + iy) * g.w + ix) * g.c + 4 * q;
+        float4* d = reinterpret_cast<float4*>(dx + idx);
         float4 o = acc[u][v];
         if (accum) {
           const float4 old = *d;
           o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
         }
         *d = o;
+        if constexpr (BNB) bnb_acc(bnb, pq, idx, o, f0, f1);
       }
     }
+    if constexpr (BNB) bnb_fold(f0, f1, s0, s1);
   }
+  if constexpr (BNB) bnb_flush(bnb, cv, s0, s1);
 }
 
 // ---- SE ----
@@ -703,9 +803,20 @@ extern "C" int pld_dwconv_fwd(const float* x, int n, int h, int w, int c, const 
                            nullptr, nullptr, 0, y, stream);
 }
 
-extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw,
-                                int k, int s, int pad_t, int pad_l, int oh, int ow, float* dx,
-                                int accumulate, void* stream) {
+// grid of a dgrad launch: with the BN epilogue a multiple of the channel-quad count's share of
+// 256 (m = cv / gcd(256, cv)), so that every thread keeps one channel quad for all its trips
+static unsigned dgrad_grid(long total, int cv, bool bnb) {
+  const unsigned g = grid_for(total);
+  if (!bnb) return g;
+  int a = 256, b = cv;
+  while (b) { const int t = a % b; a = b; b = t; }
+  const unsigned m = (unsigned)(cv / a);
+  return std::max(m, g / m * m);
+}
+
+static int dw_dgrad_impl(const float* dy, int n, int h, int w, int c, const float* wdw, int k,
+                         int s, int pad_t, int pad_l, int oh, int ow, float* dx, int accumulate,
+                         const DwBnb* bnb, unsigned* grid_out, void* stream) {
   PLD_CHECK_ARG(dy && wdw && dx && n > 0 && h > 0 && w > 0 && c > 0 && s > 0 && oh > 0 && ow > 0,
                 "pld_dwconv_dgrad: bad args");
   PLD_CHECK_ARG(c % 4 == 0, "pld_dwconv_dgrad: channels must be a multiple of 4");
@@ -716,31 +827,86 @@ extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, con
   DwGeom g = dw_geom(n, h, w, c, s, pad_t, pad_l, oh, ow);
   g.dRows = FastDiv((uint32_t)h);
   hipStream_t st = as_stream(stream);
+  const DwBnb bb = bnb ? *bnb : DwBnb{};
+  const bool B = bnb != nullptr;
   if (s == 1) {
     constexpr int T = 4, R = 4;
     const int rgroups = (h + R - 1) / R;
     g.dRows = FastDiv((uint32_t)rgroups);
     g.dTiles = FastDiv((uint32_t)((w + T - 1) / T));
     const long total = (long)n * rgroups * ((w + T - 1) / T) * (c / 4);
-    if (k == 3)
-      dwconv_dgrad_s1_kernel<3, T, R><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
-    else
-      dwconv_dgrad_s1_kernel<5, T, R><<<grid_for(total), 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    const unsigned grid = dgrad_grid(total, c / 4, B);
+    if (grid_out) *grid_out = grid;
+#define PLD_DWS1(KK)                                                                          \
+  if (B) dwconv_dgrad_s1_kernel<KK, T, R, true><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate, bb); \
+  else dwconv_dgrad_s1_kernel<KK, T, R><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+    if (k == 3) { PLD_DWS1(3) } else { PLD_DWS1(5) }
+#undef PLD_DWS1
   } else {
     const int bw = (w + 1) / 2, bh = (h + 1) / 2;
     g.dTiles = FastDiv((uint32_t)bw);
     g.dRows = FastDiv((uint32_t)bh);
-    const unsigned grid = grid_for((long)n * bh * bw * (c / 4));
+    const unsigned grid = dgrad_grid((long)n * bh * bw * (c / 4), c / 4, B);
+    if (grid_out) *grid_out = grid;
     const int par = (pad_t & 1) * 2 + (pad_l & 1);
-#define PLD_DWS2(KK)                                                                              \
-  if (par == 0) dwconv_dgrad_s2_kernel<KK, 0, 0><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
-  else if (par == 1) dwconv_dgrad_s2_kernel<KK, 0, 1><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
-  else if (par == 2) dwconv_dgrad_s2_kernel<KK, 1, 0><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate); \
-  else dwconv_dgrad_s2_kernel<KK, 1, 1><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+#define PLD_DWS2B(KK, PY, PX)                                                                   \
+  if (B) dwconv_dgrad_s2_kernel<KK, PY, PX, true><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate, bb); \
+  else dwconv_dgrad_s2_kernel<KK, PY, PX><<<grid, 256, 0, st>>>(dy, wdw, g, dx, accumulate);
+#define PLD_DWS2(KK)                                                                            \
+  if (par == 0) { PLD_DWS2B(KK, 0, 0) }                                                         \
+  else if (par == 1) { PLD_DWS2B(KK, 0, 1) }                                                    \
+  else if (par == 2) { PLD_DWS2B(KK, 1, 0) }                                                    \
+  else { PLD_DWS2B(KK, 1, 1) }
     if (k == 3) { PLD_DWS2(3) } else { PLD_DWS2(5) }
 #undef PLD_DWS2
+#undef PLD_DWS2B
   }
   return check_launch("dwconv_dgrad_kernel");
+}
+
+extern "C" int pld_dwconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wdw,
+                                int k, int s, int pad_t, int pad_l, int oh, int ow, float* dx,
+                                int accumulate, void* stream) {
+  return dw_dgrad_impl(dy, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, dx, accumulate, nullptr,
+                       nullptr, stream);
+}
+
+extern "C" size_t pld_dwconv_dgrad_bn_bwd_workspace_size(int n, int h, int w, int c, int s) {
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 || (s != 1 && s != 2)) return 0;
+  const long total = s == 1 ? (long)n * ((h + 3) / 4) * ((w + 3) / 4) * (c / 4)
+                            : (long)n * ((h + 1) / 2) * ((w + 1) / 2) * (c / 4);
+  return sizeof(double) * 2 * (size_t)c * dgrad_grid(total, c / 4, true);
+}
+
+extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
+                                  int64_t rows, int c, const float* mean, const float* invstd,
+                                  const float* gamma, const float* beta, int act,
+                                  const float* gate, const float* addn, int hw, float* dx,
+                                  int dx_accumulate, float* dgamma, float* dbeta,
+                                  int param_accumulate, float* k12, hipStream_t st);
+
+extern "C" int pld_dwconv_dgrad_bn_bwd(const float* dy, int n, int h, int w, int c,
+                                       const float* wdw, int k, int s, int pad_t, int pad_l,
+                                       int oh, int ow, float* dact, int accumulate,
+                                       const float* x, const float* mean, const float* invstd,
+                                       const float* gamma, const float* beta, int act, float* dx,
+                                       int dx_accumulate, float* dgamma, float* dbeta,
+                                       int param_accumulate, float* k12, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  PLD_CHECK_ARG(x && mean && invstd && gamma && beta && k12 && ws && aligned16(x) &&
+                    aligned16(mean) && aligned16(invstd) && aligned16(gamma) && aligned16(beta),
+                "pld_dwconv_dgrad_bn_bwd: bad BN args (16-byte aligned)");
+  const size_t need = pld_dwconv_dgrad_bn_bwd_workspace_size(n, h, w, c, s);
+  PLD_CHECK_ARG(need > 0 && ws_bytes >= need, "pld_dwconv_dgrad_bn_bwd: workspace %zu < %zu",
+                ws_bytes, need);
+  const DwBnb b{x, mean, invstd, gamma, beta, act, (double*)ws};
+  unsigned grid = 0;
+  int rc = dw_dgrad_impl(dy, n, h, w, c, wdw, k, s, pad_t, pad_l, oh, ow, dact, accumulate, &b,
+                         &grid, stream);
+  if (rc) return rc;
+  return pld__bn_bwd_finish((const double*)ws, (int)grid, x, dact, (int64_t)n * h * w, c, mean,
+                            invstd, gamma, beta, act, nullptr, nullptr, 0, dx, dx_accumulate,
+                            dgamma, dbeta, param_accumulate, k12, as_stream(stream));
 }
 
 extern "C" size_t pld_se_workspace_size(int n, int hw, int c, int cse) {

@@ -688,6 +688,23 @@ def dwconv_dgrad(dy, wdw, k, s, pad_t, pad_l, dx, accumulate=False):
                            int(accumulate), stream())
 
 
+def dwconv_dgrad_bn_bwd(dy, wdw, k, s, pad_t, pad_l, dact, x, bn, act, dgamma, dbeta, k12,
+                        dx=None, accumulate=False, dx_accumulate=False, param_accumulate=False):
+    """dwconv_dgrad into dact with the backward of the BN + act that produced the depthwise input
+    (x: that BN's input; bn = (mean, invstd, gamma, beta)) fused: its reductions in the dgrad's
+    epilogue, then dgamma/dbeta/k12, and dx (the BN input gradient) when given."""
+    n, h, w, c = dact.shape
+    _, oh, ow, _ = dy.shape
+    need = lib().pld_dwconv_dgrad_bn_bwd_workspace_size(n, h, w, c, s)
+    ws = workspace(need, "dwbnb")
+    mean, invstd, gamma, beta = bn
+    lib().pld_dwconv_dgrad_bn_bwd(ptr(dy), n, h, w, c, ptr(wdw), k, s, pad_t, pad_l, oh, ow,
+                                  ptr(dact), int(accumulate), ptr(x), ptr(mean), ptr(invstd),
+                                  ptr(gamma), ptr(beta), ACT[act], ptr(dx), int(dx_accumulate),
+                                  ptr(dgamma), ptr(dbeta), int(param_accumulate), ptr(k12),
+                                  ptr(ws), need, stream())
+
+
 def se_fwd(a, w1, b1, w2, b2, pooled, z1, gate, bn=None, act="swish"):
     """bn = (mean, invstd, gamma, beta): `a` is the pre-BN tensor; the squeeze applies BN + act."""
     n, h, w, c = a.shape

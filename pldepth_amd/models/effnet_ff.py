@@ -18,6 +18,7 @@ Data layout in HBM (one replica):
     activation are re-applied from it), plus the post-activation tensors the next op reads.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -27,6 +28,11 @@ from .engine_common import FlatStore, _BN, _Conv  # noqa: F401  (re-exported)
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.99
+# the expand BN's backward reductions in the depthwise dgrad's epilogue
+# (pld_dwconv_dgrad_bn_bwd) instead of a separate pass over (expand_pre, d act): measured no
+# faster at 448^2 batch 32 (1893 vs 1886 img/s, A/B on one box: the fused epilogue's extra
+# loads and swish' cost what the saved pass did), so off by default; PLD_DW_BNB=1 turns it on
+DW_BNB = os.environ.get("PLD_DW_BNB", "0") == "1"
 # keras.applications.efficientnet DEFAULT_BLOCKS_ARGS (B0): kernel, repeats, in, out, expand, stride
 B0_BLOCKS = [
     (3, 1, 32, 16, 1, 1),
@@ -596,21 +602,39 @@ class EffNetFF:
             ge = G[n + "expand_activation"]
             # skip taps already hold the decoder's gradient: accumulate onto it
             is_tap = n + "expand_activation" in SKIP_TAPS
-            K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
             ebn = blk["expand_bn"]
-            if blk["fused_expand_dgrad"]:
-                # the expand BN's reductions, then the expand conv's input gradient reading
-                # (expand_pre, ge) through the BN backward (pgemm): its dx is never materialised
-                k12 = self._k12_buf(blk["cexp"])
-                K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], ebn.mean,
-                                ebn.invstd, ebn.gamma, ebn.beta, "swish", ebn.dgamma, ebn.dbeta,
-                                k12)
+            bnp = (ebn.mean, ebn.invstd, ebn.gamma, ebn.beta)
+            k12 = self._k12_buf(blk["cexp"])
+            if not DW_BNB:  # A/B knob: the unfused sequence (dgrad, then the BN backward)
+                K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
+                               accumulate=is_tap)
+                if blk["fused_expand_dgrad"]:
+                    K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp,
+                                    "swish", ebn.dgamma, ebn.dbeta, k12)
+                    K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp,
+                                   "swish", k12, blk["expand"].w_dg, blk["cin"], gx_in)
+                else:
+                    gpe = self._gpre_buf(A[n + "expand_pre"].shape)
+                    ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
+                    K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
+                                               math=self._em(h, w)), gpe,
+                                   blk["expand"].w_dg, gx_in)
+            elif blk["fused_expand_dgrad"]:
+                # the depthwise dgrad gathers the expand BN's backward reductions as it stores
+                # d(expand activation) (no separate pass over (expand_pre, ge)); the expand
+                # conv's input gradient then reads (expand_pre, ge) through the BN backward
+                # (pgemm): the BN's dx is never materialised
+                K.dwconv_dgrad_bn_bwd(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
+                                      A[n + "expand_pre"], bnp, "swish", ebn.dgamma, ebn.dbeta,
+                                      k12, accumulate=is_tap)
                 K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], ebn.mean,
                                ebn.invstd, ebn.gamma, ebn.beta, "swish", k12,
                                blk["expand"].w_dg, blk["cin"], gx_in)
             else:
                 gpe = self._gpre_buf(A[n + "expand_pre"].shape)
-                ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
+                K.dwconv_dgrad_bn_bwd(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
+                                      A[n + "expand_pre"], bnp, "swish", ebn.dgamma, ebn.dbeta,
+                                      k12, dx=gpe, accumulate=is_tap)
                 K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
                                            math=self._em(h, w)), gpe,
                                blk["expand"].w_dg, gx_in)

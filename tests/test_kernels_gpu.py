@@ -984,6 +984,55 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
 
 
+@pytest.mark.parametrize("n,h,w,c,k,s,pt,pl", [(2, 13, 11, 96, 3, 1, 1, 1),
+                                                (1, 9, 10, 40, 5, 1, 2, 2),
+                                                (2, 14, 12, 1152, 3, 1, 1, 1),
+                                                (2, 15, 13, 144, 3, 2, 1, 1),
+                                                (1, 12, 14, 240, 5, 2, 1, 2)])
+def test_dwconv_dgrad_bn_bwd(cuda, n, h, w, c, k, s, pt, pl):
+    """The depthwise dgrad with the producing BN + swish's backward fused into its epilogue ==
+    pld_dwconv_dgrad then pld_bn_bwd (dx) / pld_bn_bwd_coeffs (k12), overwrite and accumulate,
+    stride 1 and 2 (both pad parities), channel quads beyond one workgroup (c = 1152)."""
+    g = torch.Generator(device=cuda).manual_seed(c + k + s)
+    oh, ow = (h + s - 1) // s, (w + s - 1) // s
+    dy = torch.randn(n, oh, ow, c, device=cuda, generator=g)
+    wdw = torch.randn(k, k, c, device=cuda, generator=g) / k
+    x = torch.randn(n, h, w, c, device=cuda, generator=g) * 2 + 0.3
+    mean = torch.randn(c, device=cuda, generator=g) * 0.2
+    invstd = torch.rand(c, device=cuda, generator=g) + 0.5
+    gamma = torch.randn(c, device=cuda, generator=g)
+    beta = torch.randn(c, device=cuda, generator=g) * 0.1
+    bnp = (mean, invstd, gamma, beta)
+    rows = n * h * w
+    for acc in (False, True):
+        pre = torch.randn(n, h, w, c, device=cuda, generator=g)
+        dact_ref = pre.clone()
+        K.dwconv_dgrad(dy, wdw, k, s, pt, pl, dact_ref, accumulate=acc)
+        dx_ref = torch.empty_like(x)
+        dg_ref, db_ref = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+        K.bn_bwd(x, dact_ref, rows, c, *bnp, "swish", dx_ref, dg_ref, db_ref)
+        k12_ref = torch.empty(2 * c, device=cuda)
+        K.bn_bwd_coeffs(x, dact_ref, rows, c, *bnp, "swish", dg_ref.clone(), db_ref.clone(),
+                        k12_ref)
+        dact = pre.clone()
+        dx = torch.empty_like(x)
+        dg, db, k12 = torch.empty(c, device=cuda), torch.empty(c, device=cuda), \
+            torch.empty(2 * c, device=cuda)
+        K.dwconv_dgrad_bn_bwd(dy, wdw, k, s, pt, pl, dact, x, bnp, "swish", dg, db, k12, dx=dx,
+                              accumulate=acc)
+        torch.cuda.synchronize()
+        assert torch.equal(dact, dact_ref)
+        for a, r in ((dg, dg_ref), (db, db_ref), (k12, k12_ref)):
+            assert rel_err(a, r) < 1e-5, rel_err(a, r)
+        assert rel_err(dx, dx_ref) < 1e-5, rel_err(dx, dx_ref)
+        # coefficients only (the pgemm_bn_bwd path)
+        dact2 = pre.clone()
+        K.dwconv_dgrad_bn_bwd(dy, wdw, k, s, pt, pl, dact2, x, bnp, "swish", dg, db, k12,
+                              accumulate=acc)
+        torch.cuda.synchronize()
+        assert torch.equal(dact2, dact_ref) and rel_err(k12, k12_ref) < 1e-5
+
+
 @pytest.mark.parametrize("math", ["bf16x3", "fp32"])
 @pytest.mark.parametrize("n,h,w,cin,c2,k,cout", [(2, 13, 11, 48, 16, 3, 72),
                                                 (1, 23, 29, 64, 0, 1, 200),
