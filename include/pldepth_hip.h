@@ -131,20 +131,6 @@ int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_ohwi, const f
                             float* y, float eps, float momentum, float* mean, float* invstd,
                             float* moving_mean, float* moving_var, void* ws, size_t ws_bytes,
                             void* stream);
-/* pld_conv2d_dgrad (single source, overwrite) into dact = the gradient at the output of a
- * BatchNormalization + activation (x = that BN's input, same shape as dact; a ResNet
- * conv{i}_block{j}_{1,2}_bn + relu, redweb.py / keras ResNet50), fused with that BN's backward:
- * its reductions (sum dz, sum dz xhat) come from the GEMM epilogue where the dgrad runs unsplit
- * on an im2col tile, else from a pld_bn_bwd / pld_bn_bwd_coeffs pass; then dgamma / dbeta
- * (param_accumulate) and, when dx != NULL, dx (the BN input gradient, dx_accumulate). k12 =
- * [mean dz | mean dz xhat] (2c floats) is written when dx == NULL or the epilogue path ran.
- * Workspace: pld_conv2d_dgrad_bn_bwd_workspace_size (the conv's own workspace stays in a->ws). */
-size_t pld_conv2d_dgrad_bn_bwd_workspace_size(const pld_conv_args* a);
-int pld_conv2d_dgrad_bn_bwd(const pld_conv_args* a, const float* dy, const float* w_dgrad,
-                            float* dact, const float* x, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, int act, float* dx,
-                            int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate,
-                            float* k12, void* ws, size_t ws_bytes, void* stream);
 
 /* number of implicit-GEMM schedules selectable through pld_conv_args.tile (FP32 math) */
 int pld_conv_num_tiles(void);

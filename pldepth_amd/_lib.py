@@ -102,9 +102,6 @@ _SIGS = {
                                       P, P, P, I32, P, F32, F32, P, P, P, P, P, SZ, P]),
     "pld_dwconv_dgrad": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, I32, P]),
     "pld_dwconv_dgrad_bn_bwd_workspace_size": (SZ, [I32, I32, I32, I32, I32]),
-    "pld_conv2d_dgrad_bn_bwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
-    "pld_conv2d_dgrad_bn_bwd": (I32, [C.POINTER(ConvArgs), P, P, P, P, P, P, P, P, I32, P, I32,
-                                      P, P, I32, P, P, SZ, P]),
     "pld_dwconv_dgrad_bn_bwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P,
                                       I32, P, P, P, P, P, I32, P, I32, P, P, I32, P, P, SZ, P]),
     "pld_se_workspace_size": (SZ, [I32, I32, I32, I32]),
@@ -142,7 +139,7 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_ti
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",
                "pld_upconv_bwd_workspace_size", "pld_se_bwd_bn_full_workspace_size",
-               "pld_dwconv_dgrad_bn_bwd_workspace_size", "pld_conv2d_dgrad_bn_bwd_workspace_size"}
+               "pld_dwconv_dgrad_bn_bwd_workspace_size"}
 
 
 def declared_symbols(header=HEADER):

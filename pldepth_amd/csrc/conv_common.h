@@ -42,15 +42,6 @@ struct GemmConvParams {
   // [N][stats_parts][2], stats_parts = M tiles x (BM / wave rows); NULL = off
   double* stats;
   int stats_parts;
-  // with bnb_x: the partials are instead the backward reductions (sum dz, sum dz xhat) of the BN
-  // + activation whose output gradient this GEMM produces (dgrad: dz = v act'(bn(x)), x = bnb_x
-  // [M][N] the BN's input, per-channel BN parameters bnb_*)
-  const float* bnb_x;
-  const float* bnb_mean;
-  const float* bnb_invstd;
-  const float* bnb_gamma;
-  const float* bnb_beta;
-  int bnb_act;
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -117,42 +108,15 @@ __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx1
       const int col = n_w + b * 32 + l32;
       const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
       double s = 0.0, q = 0.0;
-      if (p.bnb_x) {
-        const int cc = col < p.N ? col : 0;
-        const float mu = p.bnb_mean[cc], is = p.bnb_invstd[cc];
-        const float ga = p.bnb_gamma[cc], be = p.bnb_beta[cc];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          float xv[16];  // the tile's BN inputs fetched together
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            xv[r] = (row < p.M && col < p.N) ? p.bnb_x[(long)row * p.N + col] : mu;
-          }
-          float f0 = 0.f, f1 = 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float xh = (xv[r] - mu) * is;
-            const float dz = row < p.M ? (acc[a][b][r] + bias) * act_grad(p.bnb_act, xh * ga + be)
-                                       : 0.f;
-            f0 += dz;
-            f1 = fmaf(dz, xh, f1);
-          }
-          s += (double)f0;
-          q += (double)f1;
+        for (int r = 0; r < 16; ++r) {
+          const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const double v = row < p.M ? (double)(acc[a][b][r] + bias) : 0.0;
+          s += v;
+          q += v * v;
         }
-      } else {
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const double v = row < p.M ? (double)(acc[a][b][r] + bias) : 0.0;
-            s += v;
-            q += v * v;
-          }
-      }
       s += __shfl_xor(s, 32);
       q += __shfl_xor(q, 32);
       if (h == 0 && col < p.N)

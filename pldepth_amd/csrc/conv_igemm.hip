@@ -947,13 +947,6 @@ static long fwd_span_bytes(const GemmConvParams& p, int bm) {
 struct FwdStatsReq {
   double* buf = nullptr;
   int parts = 0;
-  // BN-backward reductions instead of statistics (pld_conv2d_dgrad_bn_bwd)
-  const float* bnb_x = nullptr;
-  const float* bnb_mean = nullptr;
-  const float* bnb_invstd = nullptr;
-  const float* bnb_gamma = nullptr;
-  const float* bnb_beta = nullptr;
-  int bnb_act = 0;
 };
 static thread_local FwdStatsReq g_fwd_stats;
 
@@ -961,12 +954,6 @@ static void fwd_stats_attach(GemmConvParams& p, int bm, int tm) {
   if (!g_fwd_stats.buf || p.acc1 || p.split < p.N) return;
   p.stats = g_fwd_stats.buf;
   p.stats_parts = (int)cdiv(p.M, bm) * (bm / (32 * tm));
-  p.bnb_x = g_fwd_stats.bnb_x;
-  p.bnb_mean = g_fwd_stats.bnb_mean;
-  p.bnb_invstd = g_fwd_stats.bnb_invstd;
-  p.bnb_gamma = g_fwd_stats.bnb_gamma;
-  p.bnb_beta = g_fwd_stats.bnb_beta;
-  p.bnb_act = g_fwd_stats.bnb_act;
   g_fwd_stats.parts = p.stats_parts;
 }
 
@@ -1217,63 +1204,6 @@ extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_oh
                       stream);
 }
 
-// conv dgrad + the backward of the BatchNormalization (+ activation) whose output gradient it
-// produces: the BN's reductions come from the GEMM epilogue where the dgrad runs unsplit on an
-// im2col tile (bf16x3 / fp32), else from a pld_bn_bwd / pld_bn_bwd_coeffs pass
-extern "C" size_t pld_conv2d_dgrad_bn_bwd_workspace_size(const pld_conv_args* a) {
-  if (!a || a->n <= 0 || a->h <= 0 || a->w <= 0 || a->c1 <= 0) return 0;
-  const long rows = (long)a->n * a->h * a->w;
-  const size_t gemm = sizeof(double) * 2 * (size_t)a->c1 * (cdiv(rows, 32) + 8);
-  return std::max(gemm, pld_channel_reduce_workspace_size(rows, a->c1));
-}
-
-extern "C" int pld_bn_bwd_coeffs(const float* x, const float* dy, int64_t rows, int c,
-                                 const float* mean, const float* invstd, const float* gamma,
-                                 const float* beta, int act, float* dgamma, float* dbeta,
-                                 int param_accumulate, float* k12, void* ws, void* stream);
-extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x, const float* dy,
-                                  int64_t rows, int c, const float* mean, const float* invstd,
-                                  const float* gamma, const float* beta, int act,
-                                  const float* gate, const float* addn, int hw, float* dx,
-                                  int dx_accumulate, float* dgamma, float* dbeta,
-                                  int param_accumulate, float* k12, hipStream_t st);
-
-extern "C" int pld_conv2d_dgrad_bn_bwd(const pld_conv_args* a, const float* dy,
-                                       const float* w_dgrad, float* dact, const float* x,
-                                       const float* mean, const float* invstd,
-                                       const float* gamma, const float* beta, int act, float* dx,
-                                       int dx_accumulate, float* dgamma, float* dbeta,
-                                       int param_accumulate, float* k12, void* ws,
-                                       size_t ws_bytes, void* stream) {
-  PLD_CHECK_ARG(a && a->c2 == 0 && x && mean && invstd && gamma && beta && k12 && ws,
-                "pld_conv2d_dgrad_bn_bwd: bad args (single-source conv, BN parameters, k12, ws)");
-  PLD_CHECK_ARG(ws_bytes >= pld_conv2d_dgrad_bn_bwd_workspace_size(a),
-                "pld_conv2d_dgrad_bn_bwd: workspace too small");
-  const long rows = (long)a->n * a->h * a->w;
-  FwdStatsReq req;
-  req.buf = (double*)ws;
-  req.bnb_x = x;
-  req.bnb_mean = mean;
-  req.bnb_invstd = invstd;
-  req.bnb_gamma = gamma;
-  req.bnb_beta = beta;
-  req.bnb_act = act;
-  g_fwd_stats = req;
-  int rc = pld_conv2d_dgrad(a, dy, w_dgrad, dact, 0, nullptr, 0, stream);
-  const int parts = g_fwd_stats.parts;
-  g_fwd_stats = FwdStatsReq{};
-  if (rc) return rc;
-  if (parts > 0)  // gathered by the GEMM epilogue
-    return pld__bn_bwd_finish((const double*)ws, parts, x, dact, rows, a->c1, mean, invstd, gamma,
-                              beta, act, nullptr, nullptr, 0, dx, dx_accumulate, dgamma, dbeta,
-                              param_accumulate, k12, as_stream(stream));
-  if (!dx)
-    return pld_bn_bwd_coeffs(x, dact, rows, a->c1, mean, invstd, gamma, beta, act, dgamma,
-                             dbeta, param_accumulate, k12, ws, stream);
-  return pld_bn_bwd(x, dact, rows, a->c1, mean, invstd, gamma, beta, act, nullptr, nullptr, 0,
-                    dx, dx_accumulate, dgamma, dbeta, param_accumulate, ws, stream);
-}
-
 extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
 
 extern "C" int pld_conv_num_schedules(int math) {
@@ -1427,12 +1357,8 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
     const bool vec = (p.c1 % 4 == 0) && aligned16(dy) && aligned16(w_dgrad);
     const bool vec16 = vec && (p.c1 % 16 == 0);
     hipStream_t st = as_stream(stream);
-    // the GEMM runs on the output grid: no epilogue reductions keyed by input rows here
-    const FwdStatsReq saved = g_fwd_stats;
-    g_fwd_stats = FwdStatsReq{};
     rc = run_fwd_gemm(p, vec, vec16, a->tile, (char*)a->ws + tb, a->ws_bytes - tb, st,
                       "pld_conv2d_dgrad", a->math);
-    g_fwd_stats = saved;
     if (rc) return rc;
     const long total = (long)a->n * a->h * a->w * C;
     if (C % 4 == 0 && a->c1 % 4 == 0 && aligned16(t) && aligned16(dx1) &&

@@ -446,36 +446,6 @@ def conv2d_dgrad(args, dy, w_dgrad, dx1, dx2=None, acc1=False, acc2=False):
     _end(args, tile_in)
 
 
-def conv2d_dgrad_bn_bwd(args, dy, w_dgrad, dact, x, bn, act, dgamma, dbeta, k12, dx=None,
-                        dx_accumulate=False, param_accumulate=False):
-    """conv2d_dgrad into dact (single source, overwrite) fused with the backward of the BN + act
-    whose output gradient dact is (x: that BN's input; bn = (mean, invstd, gamma, beta)): the
-    reductions from the GEMM epilogue where the dgrad's kernel gathers them, then dgamma, dbeta
-    and dx (when given; else k12)."""
-    tile_in = _begin(args)
-    _set_split(args, w_dgrad)
-    if args.tile < 0:
-        s1 = None
-
-        def run(t):
-            nonlocal s1
-            s1 = torch.empty_like(dact) if s1 is None else s1
-            args.tile = t
-            _splitk_ws(args, lib().pld_conv2d_dgrad_workspace_size)
-            lib().pld_conv2d_dgrad(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(s1), 0, None, 0,
-                                   stream())
-        args.tile = _tune("dgrad", args, run)
-    _splitk_ws(args, lib().pld_conv2d_dgrad_workspace_size)
-    need = lib().pld_conv2d_dgrad_bn_bwd_workspace_size(C.byref(args))
-    ws = workspace(need, "dgbnb")
-    mean, invstd, gamma, beta = bn
-    lib().pld_conv2d_dgrad_bn_bwd(C.byref(args), ptr(dy), ptr(w_dgrad), ptr(dact), ptr(x),
-                                  ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ACT[act],
-                                  ptr(dx), int(dx_accumulate), ptr(dgamma), ptr(dbeta),
-                                  int(param_accumulate), ptr(k12), ptr(ws), need, stream())
-    _end(args, tile_in)
-
-
 def conv2d_wgrad(args, dy, dw, accumulate=False):
     tile_in = _begin(args)
     if args.tile < 0:

@@ -20,7 +20,6 @@ it), each post-activation tensor a later op reads, and one gradient buffer per a
 The encoder convs need dX only (frozen), the stem conv neither dX nor dW.
 """
 import math
-import os
 
 import numpy as np
 import torch
@@ -29,11 +28,6 @@ from .. import kernels as K
 from .engine_common import FlatStore, _BN, _Conv
 
 RESNET_BN_EPS = 1.001e-5
-# BN-backward reductions from the producing dgrad's GEMM epilogue (pld_conv2d_dgrad_bn_bwd)
-# instead of a separate pass: measured equal at 448^2 batch 32 (824 / 826 vs 823 / 828 img/s,
-# A/B on one box — many of these dgrads run on the wide / thin 1x1 or split-K paths, which keep
-# the pass), so off by default; PLD_DGRAD_BNB=1 turns it on
-DGRAD_BNB = os.environ.get("PLD_DGRAD_BNB", "0") == "1"
 CAFFE_MEAN_BGR = np.array([103.939, 116.779, 123.68], np.float32)
 RESNET50_STACKS = [("conv2", 64, 3, 1), ("conv3", 128, 4, 2), ("conv4", 256, 6, 2),
                    ("conv5", 512, 3, 2)]
@@ -344,10 +338,8 @@ class RedWebFF:
         return A[n + "/out"]
 
     # ------------------------------------------------------------------ backward
-    def _wgrad_dgrad(self, conv, x, gy, h, w, oh, ow, gx, gx_acc=False, bnb=None):
-        """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given. bnb = (bn, x_pre,
-        act, g_pre): gx is the gradient at that BN + act's output; its backward follows, with
-        the reductions from the dgrad's GEMM epilogue where the kernel gathers them."""
+    def _wgrad_dgrad(self, conv, x, gy, h, w, oh, ow, gx, gx_acc=False):
+        """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given."""
         k, s = conv.k, conv.stride
         pt = pl = ((k - 1) // 2 if s == 1 else 0)
         args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout,
@@ -356,25 +348,8 @@ class RedWebFF:
             K.conv2d_wgrad(args, gy, conv.dw)
             if conv.db is not None:
                 K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db)
-        if gx is None:
-            return
-        if bnb is not None and DGRAD_BNB and not gx_acc:
-            bn, x_pre, act, g_pre = bnb
-            K.conv2d_dgrad_bn_bwd(args, gy, conv.w_dg, gx, x_pre,
-                                  (bn.mean, bn.invstd, bn.gamma, bn.beta), act, bn.dgamma,
-                                  bn.dbeta, self._k12_buf(bn.c), dx=g_pre)
-            return
-        K.conv2d_dgrad(args, gy, conv.w_dg, gx, None, acc1=gx_acc)
-        if bnb is not None:
-            bn, x_pre, act, g_pre = bnb
-            bn.bwd(x_pre, gx, x_pre.numel() // bn.c, act, g_pre)
-
-    def _k12_buf(self, c):
-        if not hasattr(self, "_k12"):
-            self._k12 = {}
-        if c not in self._k12:
-            self._k12[c] = torch.empty(2 * c, device=self.device)
-        return self._k12[c]
+        if gx is not None:
+            K.conv2d_dgrad(args, gy, conv.w_dg, gx, None, acc1=gx_acc)
 
     def param_offset(self, name):
         """Offset of a trainable tensor in the flat params / grads buffers."""
@@ -428,12 +403,12 @@ class RedWebFF:
         else:
             blk["bn3"].add_bwd(A[n + "3_pre"], gout, rows, x, "relu", g3, gx,
                                dres_acc=gx_is_tap)
+        self._wgrad_dgrad(blk["c3"], A[n + "2_relu"], g3, oh, ow, oh, ow, G[n + "2_relu"])
         g2 = self._gpre_buf(A[n + "2_pre"].shape, 1)
-        self._wgrad_dgrad(blk["c3"], A[n + "2_relu"], g3, oh, ow, oh, ow, G[n + "2_relu"],
-                          bnb=(blk["bn2"], A[n + "2_pre"], "relu", g2))
+        blk["bn2"].bwd(A[n + "2_pre"], G[n + "2_relu"], rows, "relu", g2)
+        self._wgrad_dgrad(blk["c2"], A[n + "1_relu"], g2, oh, ow, oh, ow, G[n + "1_relu"])
         g1 = self._gpre_buf(A[n + "1_pre"].shape, 1)
-        self._wgrad_dgrad(blk["c2"], A[n + "1_relu"], g2, oh, ow, oh, ow, G[n + "1_relu"],
-                          bnb=(blk["bn1"], A[n + "1_pre"], "relu", g1))
+        blk["bn1"].bwd(A[n + "1_pre"], G[n + "1_relu"], rows, "relu", g1)
         if blk["proj"]:
             g0 = self._gpre_buf(A[n + "0_pre"].shape)
             blk["bn0"].bwd(A[n + "0_pre"], gsc, rows, "none", g0)
@@ -450,14 +425,14 @@ class RedWebFF:
             gin = gx if half == 0 else G[f"{n}/out0"]
             gp = self._gpre_buf(A[f"{n}/pre{half + 2}"].shape)
             b[half + 2].add_bwd(A[f"{n}/pre{half + 2}"], gy, rows, xin, "relu", gp, gin)
-            gq = self._gpre_buf(A[f"{n}/pre{half + 1}"].shape)
             self._wgrad_dgrad(c[half + 2], A[f"{n}/act{half + 1}"], gp, h, w, h, w,
-                              G[f"{n}/act{half + 1}"],
-                              bnb=(b[half + 1], A[f"{n}/pre{half + 1}"], "relu", gq))
-            gq0 = self._gpre_buf(A[f"{n}/pre{half}"].shape, 1)
+                              G[f"{n}/act{half + 1}"])
+            gq = self._gpre_buf(A[f"{n}/pre{half + 1}"].shape)
+            b[half + 1].bwd(A[f"{n}/pre{half + 1}"], G[f"{n}/act{half + 1}"], rows, "relu", gq)
             self._wgrad_dgrad(c[half + 1], A[f"{n}/act{half}"], gq, h, w, h, w,
-                              G[f"{n}/act{half}"],
-                              bnb=(b[half], A[f"{n}/pre{half}"], "relu", gq0))
+                              G[f"{n}/act{half}"])
+            gq0 = self._gpre_buf(A[f"{n}/pre{half}"].shape, 1)
+            b[half].bwd(A[f"{n}/pre{half}"], G[f"{n}/act{half}"], rows, "relu", gq0)
             self._wgrad_dgrad(c[half], xin, gq0, h, w, h, w, gin, gx_acc=True)
             gy = gin
 

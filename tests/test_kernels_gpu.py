@@ -984,47 +984,6 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
         assert rel_err(a, b) < 1e-6, rel_err(a, b)
 
 
-@pytest.mark.parametrize("math", ["bf16x3", "fp32"])
-@pytest.mark.parametrize("n,h,w,c,k,cout", [(2, 13, 11, 64, 3, 48), (1, 9, 10, 96, 1, 384)])
-def test_conv_dgrad_bn_bwd(cuda, math, n, h, w, c, k, cout):
-    """pld_conv2d_dgrad_bn_bwd (the BN's backward reductions from the dgrad GEMM epilogue on
-    unsplit im2col schedules, a pld_bn_bwd pass elsewhere) == pld_conv2d_dgrad + pld_bn_bwd /
-    pld_bn_bwd_coeffs, on every schedule; ragged M tiles."""
-    g = torch.Generator(device=cuda).manual_seed(c + k + cout)
-    x_in = torch.randn(n, h, w, c, device=cuda, generator=g)  # the conv input (geometry only)
-    wt = torch.randn(k, k, c, cout, device=cuda, generator=g) / (k * k * c) ** 0.5
-    wd = K.filter_to_dgrad(wt)
-    dy = torch.randn(n, h, w, cout, device=cuda, generator=g)
-    xb = torch.randn(n, h, w, c, device=cuda, generator=g) * 1.5 + 0.2  # the BN's input
-    bnp = (torch.randn(c, device=cuda, generator=g) * 0.2,
-           torch.rand(c, device=cuda, generator=g) + 0.5,
-           torch.randn(c, device=cuda, generator=g), torch.randn(c, device=cuda, generator=g))
-    rows = n * h * w
-    p = (k - 1) // 2
-    for t in range(_lib.lib().pld_conv_num_schedules(K.MATH[math])):
-        args = K.conv_args(x_in, None, k, k, 1, p, p, h, w, cout, math=math)
-        args.tile = t
-        dact_ref = torch.empty_like(xb)
-        K.conv2d_dgrad(args, dy, wd, dact_ref)
-        dx_ref = torch.empty_like(xb)
-        dg_ref, db_ref = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
-        K.bn_bwd(xb, dact_ref, rows, c, *bnp, "relu", dx_ref, dg_ref, db_ref)
-        k12_ref = torch.empty(2 * c, device=cuda)
-        K.bn_bwd_coeffs(xb, dact_ref, rows, c, *bnp, "relu", dg_ref.clone(), db_ref.clone(),
-                        k12_ref)
-        dact, dx = torch.empty_like(xb), torch.empty_like(xb)
-        dg, db, k12 = (torch.empty(c, device=cuda), torch.empty(c, device=cuda),
-                       torch.empty(2 * c, device=cuda))
-        K.conv2d_dgrad_bn_bwd(args, dy, wd, dact, xb, bnp, "relu", dg, db, k12, dx=dx)
-        torch.cuda.synchronize()
-        assert torch.equal(dact, dact_ref), t
-        for a, r in ((dg, dg_ref), (db, db_ref), (dx, dx_ref)):
-            assert rel_err(a, r) < 1e-5, (t, rel_err(a, r))
-        K.conv2d_dgrad_bn_bwd(args, dy, wd, dact, xb, bnp, "relu", dg, db, k12)
-        torch.cuda.synchronize()
-        assert rel_err(k12, k12_ref) < 1e-5, t
-
-
 @pytest.mark.parametrize("n,h,w,c,k,s,pt,pl", [(2, 13, 11, 96, 3, 1, 1, 1),
                                                 (1, 9, 10, 40, 5, 1, 2, 2),
                                                 (2, 14, 12, 1152, 3, 1, 1, 1),
