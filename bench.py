@@ -278,6 +278,53 @@ def cpu_baseline(H, W, L, R, model="ff_effnet", seconds_budget=25.0):
                       f"{H}x{W}, L={L}, R={R}, torch.set_num_threads(8)"}
 
 
+def loss_parity(tr, lr, threads=16):
+    """The metric's second half, "ListMLE loss delta vs TF2": one more step of the benchmark's
+    own trainer (eager, same batch, the next step's sampler rankings and drop-connect masks),
+    and the oracle's fp64 restatement of the reference forward (oracle/effnet.py or
+    oracle/redweb.py, training-mode BN, the step's drop-connect scales injected) + ListMLE
+    (oracle/listmle.py: depth_utils.py:39-61 + tfr ListMLE) on the same weights, images and
+    y_true. Checker only: rank 0 at N=1, after the timed region, like cpu_baseline()."""
+    sys.path.insert(0, ROOT)
+    from oracle import listmle as LM
+    eng = tr.engine
+    weights = eng.get_weights()  # the weights this step's forward runs with
+    tr.step_eager(lr)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    loss = tr.loss_value()
+    pred = eng.act["pred"].double().cpu()
+    x = eng.act["input"].double().cpu()
+    y = tr.y_true.cpu().numpy()
+    B, R, L = y.shape[0], y.shape[1], y.shape[2]
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(threads, len(os.sched_getaffinity(0)))))
+    t0 = time.perf_counter()
+    try:
+        with torch.no_grad():
+            if eng.__class__.__name__ == "RedWebFF":
+                from oracle import redweb as OR
+                pred_ref = OR.forward(P, x, preprocessed=True)
+            else:
+                from oracle import effnet as OE
+                drop = {blk["name"]: blk["drop"].double().cpu() for blk in eng.blocks
+                        if blk.get("residual") and blk.get("rate", 0) > 0 and eng.drop_connect}
+                pred_ref = OE.forward(P, x, drop_scales=drop or None)
+    finally:
+        torch.set_num_threads(nthreads)
+    loss_ref, _ = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
+    return {
+        "loss": loss, "loss_oracle_fp64": float(loss_ref),
+        "loss_delta": abs(loss - loss_ref) / abs(loss_ref),
+        "pred_delta": float((pred - pred_ref).abs().max() / pred_ref.abs().max()),
+        "lists": B * R, "oracle_seconds": round(time.perf_counter() - t0, 1),
+        "how": "one extra eager step of the bench trainer (its own batch, sampler rankings and "
+               "drop-connect masks) vs the fp64 oracle forward + ListMLE on the same weights; "
+               "delta = |loss - oracle| / |oracle|, pred_delta = max|dpred| / max|pred|",
+    }
+
+
 def _cpu_weights(H, W):
     # the engine's initialiser, run on CPU buffers (no GPU needed)
     from pldepth_amd.models import effnet_ff as E
@@ -364,8 +411,15 @@ def main():
     ap.add_argument("--sampling-type", type=int, default=1)
     ap.add_argument("--model", default="ff_effnet", choices=["ff_effnet", "ff_redweb"],
                     help="ff_redweb = the ResNet-50 backbone (BASELINE cfg3 'ff_resnet')")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="step eagerly (no hipGraph capture): the host-launch-bound comparison")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo rehearses the "
+                         "path with ranks sharing one GPU)")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU legs (cpu_baseline timing and the loss-delta check)")
+    ap.add_argument("--no-loss-parity", action="store_true",
+                    help="skip the ListMLE loss delta vs the fp64 oracle (loss_parity)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the cfg3 (ff_resnet) and cfg5 (L=64, R=1000) lines (1 GPU only)")
     ap.add_argument("--conv-math", default="auto", choices=["auto", "mixed", "bf16x3", "fp32"],
@@ -384,12 +438,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world}"
-    torch.cuda.set_device(local)
+    # one rank per GPU; ranks beyond the visible GPUs share them (the gloo rehearsal of the
+    # N > 1 path on a 1-GPU box: tests/test_bench_gpu.py)
+    dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if a.backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(a.backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
 
     from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
@@ -433,12 +493,17 @@ def main():
         "config": {"workload": workload,
                    "model": a.model, "global_batch": world * B, "input": f"{H}x{H}",
                    "ranking_size": L, "rankings_per_image": R,
-                   "parallelism": f"dp{world}", "graph": not a.no_graph},
+                   "parallelism": f"dp{world}", "graph": not a.no_graph,
+                   "backend": a.backend if world > 1 else None},
         "conv_math": {"policy": a.conv_math, "encoder": tr.engine.enc_math,
                       "decoder": tr.engine.dec_math},
         "roofline": roof,
         "loss": loss,
     }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.no_loss_parity:
+        par = loss_parity(tr, 0.01)
+        out["loss_delta"] = par["loss_delta"]
+        out["loss_parity"] = par
     del tr
     if world == 1 and not a.no_extra_configs and a.model == "ff_effnet" and H == 448:
         extra = {}

@@ -12,6 +12,7 @@ Differences from the reference driver, all outside the accelerated path (SURVEY 
 Everything per step — sampling, forward, ListMLE, backward, Adam-AMSGrad — runs on the GPU.
 """
 import json
+import os
 import time
 
 import click
@@ -160,7 +161,7 @@ def perform_pldepth_experiment(model_name, epochs, batch_size, seed, ranking_siz
               validation_data=val_ds, verbose=1)
     if save_path:  # PLDepth.py:180-181: weights, plus the whole model as .h5
         model.save_weights(save_path)
-        model.save(save_path.rsplit(".", 1)[0] + "_model.h5")
+        model.save(os.path.splitext(save_path)[0] + "_model.h5")
     # test pass (PLDepth.py:183-192): ordinal error and nDCG@200 on the first 250 images of the
     # held-out eval split, on the GPU (pldepth_amd.active_learning.metrics). Like the reference,
     # the images go in raw (no preprocess_fn: PLDepth.py:187-191 calls calc_err / dcg_metric on

@@ -92,15 +92,37 @@ class Graph:
         self.exec = None
 
     def capture(self, fn):
-        lib().pld_graph_begin(stream())
-        _CAPTURING[0] = True
-        _LIVE_GRAPHS[0] += 1
+        self.begin()
         try:
             fn()
-        finally:
-            _CAPTURING[0] = False
-            h = C.c_void_p()
+        except BaseException:
+            self.end(failed=True)
+            raise
+        return self.end()
+
+    def begin(self):
+        """Start capturing the current stream (every launch until end() joins the graph)."""
+        lib().pld_graph_begin(stream())
+        _CAPTURING[0] = True
+        # workspaces superseded during capture are retired from here on (the graph being built
+        # may hold their pointers); the count stays only if the graph is instantiated
+        _LIVE_GRAPHS[0] += 1
+        return self
+
+    def end(self, failed=False):
+        _CAPTURING[0] = False
+        h = C.c_void_p()
+        try:
             lib().pld_graph_end(stream(), C.byref(h))
+        except BaseException:
+            _LIVE_GRAPHS[0] -= 1
+            if failed:
+                return self  # the capture's own exception is the one to report
+            raise
+        if failed:
+            lib().pld_graph_destroy(h)
+            _LIVE_GRAPHS[0] -= 1
+            return self
         self.exec = h
         return self
 

@@ -68,6 +68,8 @@ class RedWebFF:
         self.init_weights(seed)
         self._alloc()
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
+        # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
+        self.exact_stages = ()
         self.seed = seed
 
     preprocess = staticmethod(preprocess_input)
@@ -234,6 +236,8 @@ class RedWebFF:
     def _math(self, conv, oh=None, ow=None):
         if conv.trainable:
             return self.dec_math
+        if self.enc_math == "auto" and conv.name.startswith(self.exact_stages):
+            return "fp32"
         # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
         return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
                               getattr(self, "x3_min_population", None))
@@ -261,8 +265,7 @@ class RedWebFF:
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
         args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64,
-                           math=K.encoder_math(self.enc_math, B * h * w,
-                                               getattr(self, "x3_min_population", None)))
+                           math=self._math(self.stem, h, w))
         self.stem_bn.conv_fwd_stats(args, self.stem.w_nat, self.stem.b, A["conv1_pre"], B * h * w,
                                     training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)

@@ -9,19 +9,24 @@ all-reduce the reference never had: one process per GPU, torch.di
 semantics), one fp32 all-reduce of the flat gradient buffer, 1/world folded into Adam.
 
 Stepping: the whole step is stream-ordered HIP work with no host synchronisation. N = 1: one
-hipGraph per step (captured after a first eager step). N > 1: eager launches (the host issues a
-step in less time than the GPU runs it: graph and eager steps measure the same throughput), with
-the gradient exchange overlapped with the backward: the backward reports, layer by layer, which
-tail of the flat gradient buffer is final (engine.backward(grad_ready=...)); each ~8 MB bucket
-is all-reduced asynchronously as it completes (RCCL on its own stream) and a side stream runs
-that bucket's Adam-AMSGrad + filter refresh as soon as it lands, while the compute stream carries
-on with the rest of the backward (the decoder holds 99.6 % of the gradient bytes and finishes
-before the encoder backward starts). Per-step scalars (learning rate, step counter) live in
-device memory.
+hipGraph per step (captured after a first eager step). N > 1: the gradient exchange overlaps the
+backward: the backward reports, layer by layer, which tail of the flat gradient buffer is final
+(engine.backward(grad_ready=...)); each ~8 MB bucket is all-reduced asynchronously as it
+completes (RCCL on its own stream) and a side stream runs that bucket's Adam-AMSGrad + filter
+refresh as soon as it lands, while the compute stream carries on with the rest of the backward
+(the decoder holds 99.6 % of the gradient bytes and finishes before the encoder backward
+starts). The N > 1 step is captured too, in segments: the compute stream's work between two
+bucket boundaries is one hipGraph, each bucket's update another (on the side stream); a replay
+launches the segment graphs and, between them, issues the bucket all-reduces through
+torch.distributed (the collectives stay outside the graphs: RCCL's own stream, c10d's stream
+dependencies and its work objects run as they do eagerly). Per step the host then issues
+~2 graph launches + 1 collective per bucket instead of ~500 kernel launches. Per-step scalars
+(learning rate, step counter) live in device memory.
 """
 import numpy as np
 import torch
 
+from . import dp
 from . import kernels as K
 from .models.effnet_ff import EffNetFF
 from .models.redweb_ff import RedWebFF
@@ -156,31 +161,31 @@ class ReplicaTrainer:
         eng = self.engine
         return [c for c in eng.convs if c.trainable and lo <= eng.param_offset(c.wk) < hi]
 
+    def _dp_update(self, lo, hi):
+        """Adam-AMSGrad of flat range [lo, hi) (grad_scale 1/world) and the refresh of the
+        native filter copies of the convs in it, on the current (side) stream."""
+        eng = self.engine
+        b1, b2, eps = self.betas
+        K.adam_amsgrad_dev(eng.params.buf[lo:hi], eng.grads.buf[lo:hi], self.m[lo:hi],
+                           self.v[lo:hi], self.vhat[lo:hi], self.lr_dev, self.step_dev, b1, b2,
+                           eps, grad_scale=1.0 / self.world)
+        for c in self._dp_refresh_convs(lo, hi):
+            c.refresh()
+
     def _dp_bucket(self, lo, hi):
         """All-reduce grads[lo:hi) (async, ordered after the compute stream's work so far), then
-        on the side stream: wait for it, Adam-AMSGrad of that range (grad_scale 1/world), refresh
-        of the native filter copies of the convs in it."""
-        import torch.distributed as dist
-        eng = self.engine
-        g = eng.grads.buf[lo:hi]
-        work = dist.all_reduce(g, group=self.pg, async_op=True)
-        b1, b2, eps = self.betas
+        on the side stream: wait for it and run the bucket's update."""
+        work = dp.allreduce_bucket(self.engine.grads.buf, lo, hi, self.pg)
         with torch.cuda.stream(self.side):
             work.wait()
-            K.adam_amsgrad_dev(eng.params.buf[lo:hi], g, self.m[lo:hi], self.v[lo:hi],
-                               self.vhat[lo:hi], self.lr_dev, self.step_dev, b1, b2, eps,
-                               grad_scale=1.0 / self.world)
-            for c in self._dp_refresh_convs(lo, hi):
-                c.refresh()
+            self._dp_update(lo, hi)
         self._dp_works.append(work)
 
     def _dp_grad_ready(self, off):
-        """engine.backward hook: grads[off:] are final. Launch a bucket once >= BUCKET_BYTES are
-        pending, and always for the last (offset 0) call."""
-        pending = (self._dp_hi - off) * 4
-        if off < self._dp_hi and (pending >= self.BUCKET_BYTES or off == 0):
-            self._dp_bucket(off, self._dp_hi)
-            self._dp_hi = off
+        """engine.backward hook: grads[off:] are final (dp.BucketSchedule decides)."""
+        b = self._dp_sched.ready(off)
+        if b is not None:
+            self._dp_bucket(*b)
 
     def _step_dp(self):
         """One data-parallel step (N > 1), eager, on self.stream (+ RCCL and the side stream)."""
@@ -190,11 +195,69 @@ class ReplicaTrainer:
         K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
                           dpred=self.dpred, nll=self.nll, loss=self.loss, zero_dpred=True)
         self.side.wait_stream(self.stream)
-        self._dp_hi, self._dp_works = eng.grads.buf.numel(), []
+        self._dp_sched = dp.BucketSchedule(eng.grads.buf.numel(), self.BUCKET_BYTES)
+        self._dp_works = []
         eng.backward(self.dpred, grad_ready=self._dp_grad_ready)
         self._dp_grad_ready(0)
         # the step counter (Adam's bias correction, the next step's Philox keys) advances once
         # every bucket's update has run; the next step's forward reads the updated filters
+        self.stream.wait_stream(self.side)
+        K.step_increment(self.step_dev)
+
+    def _capture_dp(self):
+        """Segmented capture of the N > 1 step (module docstring): the compute stream's launches
+        from the step start to the first bucket boundary, between boundaries, up to the last
+        one (offset 0: the end of the backward) are graphs `segs`; each bucket's Adam-AMSGrad +
+        filter refresh on the side stream is a graph in `bucket_graphs`."""
+        eng = self.engine
+        torch.cuda.synchronize()
+        segs, buckets = [], []
+        sched = dp.BucketSchedule(eng.grads.buf.numel(), self.BUCKET_BYTES)
+        cur = [None]
+
+        def boundary(off):
+            b = sched.ready(off)
+            if b is not None:
+                segs.append(cur[0].end())
+                buckets.append(b)
+                cur[0] = None if sched.done else K.Graph().begin()
+
+        with torch.cuda.stream(self.stream):
+            cur[0] = K.Graph().begin()
+            try:
+                self._sample()
+                eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
+                K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
+                                  dpred=self.dpred, nll=self.nll, loss=self.loss,
+                                  zero_dpred=True)
+                eng.backward(self.dpred, grad_ready=boundary)
+                boundary(0)
+            except BaseException:
+                if cur[0] is not None:
+                    cur[0].end(failed=True)
+                raise
+        assert sched.done and len(segs) == len(buckets), "backward never reached offset 0"
+        with torch.cuda.stream(self.side):
+            graphs = [K.Graph().capture(lambda lo=lo, hi=hi: self._dp_update(lo, hi))
+                      for lo, hi in buckets]
+        torch.cuda.synchronize()
+        self.graphs = segs
+        self.bucket_graphs = list(zip(buckets, graphs))
+
+    def _replay_dp(self):
+        """One captured N > 1 step on self.stream (the caller's current stream)."""
+        eng = self.engine
+        self.side.wait_stream(self.stream)
+        works = []
+        for seg, ((lo, hi), upd) in zip(self.graphs, self.bucket_graphs):
+            seg.launch()
+            # c10d orders the collective after the current stream (self.stream) = this segment
+            work = dp.allreduce_bucket(eng.grads.buf, lo, hi, self.pg)
+            with torch.cuda.stream(self.side):
+                work.wait()
+                upd.launch()
+            works.append(work)
+        self._dp_works = works
         self.stream.wait_stream(self.side)
         K.step_increment(self.step_dev)
 
@@ -220,7 +283,8 @@ class ReplicaTrainer:
                           "the first GPU call (see pldepth_amd/__init__.py); stepping eagerly")
             return
         if self.world > 1:
-            return  # data-parallel steps stay eager (see the module docstring)
+            self._capture_dp()
+            return
         torch.cuda.synchronize()
         with torch.cuda.stream(self.stream):
             g = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd(), self._update()))
@@ -232,6 +296,9 @@ class ReplicaTrainer:
             return self.step_eager(lr)
         with torch.cuda.stream(self.stream):
             K.set_scalar(self.lr_dev, lr)
+            if self.world > 1:
+                self._replay_dp()
+                return
             self.graphs[0].launch()
 
     def loss_value(self):

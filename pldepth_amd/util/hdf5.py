@@ -12,15 +12,21 @@ writer — the layout libhdf5 produces with its default ("earliest") format, whi
 reader — the same plus what newer libraries write for such files: superblock versions 0-3,
   object header versions 1 and 2 with continuation blocks, compact (link-message) groups,
   attribute messages versions 1-3, dataspace versions 1-2, contiguous and compact layouts
-  (layout message versions 1-4), fixed-point / floating-point / fixed-length string datatypes.
-  Dense (fractal-heap) link or attribute storage, chunked or filtered datasets and variable-
-  length strings raise NotImplementedError (Keras' HDF5 weight files use none of them).
+  (layout message versions 1-4), fixed-point / floating-point / fixed-length string datatypes,
+  and variable-length strings (datatype class 9, the elements in global-heap collections): what
+  h5py stores for a Python ``str`` attribute (h5py 2.10 under Keras writes e.g. the root
+  ``keras_version`` / ``backend`` that way when handed str). The writer emits them for
+  ``VLenStr`` values (so tests can build such files). Dense (fractal-heap) link or attribute
+  storage and chunked or filtered datasets raise NotImplementedError (Keras' HDF5 weight files
+  use none of them); an attribute of an unsupported datatype is skipped with a warning instead
+  of failing the whole load.
 
 In memory a file is a tree of ``Group`` (``attrs`` + ordered members) and ``Dataset``
 (``data`` numpy array + ``attrs``). Paths with '/' create / look up nested groups like h5py.
 Parity with h5py-written files is unpinned: no HDF5 library exists here to produce or check one.
 """
 import struct
+import warnings
 
 import numpy as np
 
@@ -28,6 +34,19 @@ SIGNATURE = b"\x89HDF\r\n\x1a\n"
 UNDEF = 0xFFFFFFFFFFFFFFFF
 GROUP_INTERNAL_K = 16
 LOCAL_HEAP_FREE_NULL = 1  # libhdf5's end-of-free-list marker for local heaps
+GLOBAL_HEAP_MIN = 4096  # libhdf5's smallest global-heap collection (H5HG_MINSIZE)
+
+
+class VLenStr(str):
+    """A str attribute value written as an HDF5 variable-length UTF-8 string (h5py's encoding of
+    a Python str) instead of a fixed-length one."""
+
+
+class _VLen(object):
+    """Decoded class-9 datatype: a variable-length string (or sequence of `base`)."""
+
+    def __init__(self, is_str, base, size):
+        self.is_str, self.base, self.itemsize = is_str, base, size
 
 
 class Dataset(object):
@@ -151,13 +170,44 @@ def _message(mtype, body, flags=0):
     return struct.pack("<HHB3x", mtype, len(body), flags) + body
 
 
-def _attribute_message(name, value):
-    a = _as_storable(value)
+def _vlen_str_dtype_message():
+    """Class 9 (variable-length) version 1: type 1 = string, padding 0 = null-terminated,
+    character set 1 = UTF-8; element size 16 (u32 length + global heap id: u64 collection
+    address + u32 object index); base type: 1-byte unsigned fixed-point (libhdf5's parent type
+    of a variable-length string)."""
+    return struct.pack("<BBBBI", (1 << 4) | 9, 0x01, 0x01, 0, 16) + \
+        struct.pack("<BBBBI", (1 << 4) | 0, 0, 0, 0, 1) + struct.pack("<HH", 0, 8)
+
+
+def _global_heap_collection(objects):
+    """A global heap collection ("GCOL", version 1) holding `objects` (bytes) at indices
+    1..n, then the free-space object (index 0) covering the rest of the >= 4 KiB collection."""
+    body = b""
+    for i, data in enumerate(objects, 1):
+        body += struct.pack("<HH4xQ", i, 1, len(data)) + _pad8(data)
+    size = 16 + len(body) + 16
+    size = max(size, GLOBAL_HEAP_MIN)
+    size += -size % 8
+    free = size - 16 - len(body)
+    body += struct.pack("<HH4xQ", 0, 0, free) + b"\0" * (free - 16)
+    return b"GCOL" + struct.pack("<B3xQ", 1, size) + body
+
+
+def _attribute_message(name, value, writer=None):
     nm = name.encode("utf8") + b"\0"
-    dtm = _dtype_message(a.dtype)
-    dsm = _dataspace_message(a.shape)
+    if isinstance(value, VLenStr):
+        if writer is None:
+            raise ValueError("variable-length strings need the file writer (global heap)")
+        data = value.encode("utf8")
+        coll = writer.alloc(_global_heap_collection([data]))
+        dtm, dsm = _vlen_str_dtype_message(), _dataspace_message(())
+        raw = struct.pack("<IQI", len(data), coll, 1)
+    else:
+        a = _as_storable(value)
+        dtm, dsm = _dtype_message(a.dtype), _dataspace_message(a.shape)
+        raw = np.ascontiguousarray(a).tobytes()
     body = struct.pack("<BBHHH", 1, 0, len(nm), len(dtm), len(dsm))
-    body += _pad8(nm) + _pad8(dtm) + _pad8(dsm) + np.ascontiguousarray(a).tobytes()
+    body += _pad8(nm) + _pad8(dtm) + _pad8(dsm) + raw
     return _message(0x000C, body)
 
 
@@ -188,7 +238,7 @@ class _Writer(object):
                 _message(0x0003, _dtype_message(a.dtype), flags=1),  # constant
                 _message(0x0005, struct.pack("<BBBB", 2, 1, 2, 0)),   # fill value: undefined
                 _message(0x0008, struct.pack("<BBQQ", 3, 1, addr, len(raw)))]
-        msgs += [_attribute_message(k, v) for k, v in ds.attrs.items()]
+        msgs += [_attribute_message(k, v, self) for k, v in ds.attrs.items()]
         return self.object_header(msgs)
 
     def group(self, g, leaf_k):
@@ -237,7 +287,7 @@ class _Writer(object):
         bt += struct.pack("<Q", keys[nchild] if nchild < len(keys) else 0)
         bt_addr = self.alloc(bt)
         msgs = [_message(0x0011, struct.pack("<QQ", bt_addr, heap_addr))]
-        msgs += [_attribute_message(k, v) for k, v in g.attrs.items()]
+        msgs += [_attribute_message(k, v, self) for k, v in g.attrs.items()]
         return self.object_header(msgs), bt_addr, heap_addr
 
 
@@ -355,7 +405,45 @@ class _Reader(object):
             return np.dtype(f"{bo}f{size}"), 8 + 12
         if cls == 3:
             return np.dtype(f"S{size}"), 8
+        if cls == 9:
+            base, blen = self.dtype(m[8:])
+            return _VLen((bf0 & 0x0F) == 1, base, size), 8 + blen
         raise NotImplementedError(f"HDF5 datatype class {cls} (version {ver})")
+
+    def global_heap_object(self, coll, index):
+        b, p = self.b, self.base + coll
+        if b[p:p + 4] != b"GCOL":
+            raise ValueError("bad global heap collection")
+        size = struct.unpack_from("<Q", b, p + 8)[0]
+        q, end = p + 16, p + size
+        while q + 16 <= end:
+            idx, _, osz = struct.unpack_from("<HH4xQ", b, q)
+            if idx == index:
+                return bytes(b[q + 16:q + 16 + osz])
+            if idx == 0:
+                break
+            q += 16 + osz + (-osz % 8)
+        raise ValueError(f"global heap object {index} not found in collection at {coll}")
+
+    def decode_vlen(self, vt, raw, shape):
+        """Elements of a class-9 datatype: 16-byte (length, collection, index) records."""
+        n = int(np.prod(shape)) if shape else 1
+        vals = []
+        for i in range(n):
+            ln, coll, idx = struct.unpack_from("<IQI", raw, 16 * i)
+            if coll in (0, UNDEF) or ln == 0:
+                data = b""
+            else:
+                data = self.global_heap_object(coll, idx)
+            if vt.is_str:
+                vals.append(data[:ln].split(b"\0")[0].decode("utf8", errors="replace"))
+            else:
+                vals.append(np.frombuffer(data, vt.base, ln).copy())
+        if not shape:
+            return vals[0]
+        out = np.empty(n, dtype=object)
+        out[:] = vals
+        return out.reshape(shape)
 
     @staticmethod
     def dataspace(m):
@@ -399,10 +487,15 @@ class _Reader(object):
         if shape is None:
             return name, None
         n = int(np.prod(shape)) if shape else 1
+        if isinstance(dt, _VLen):
+            return name, self.decode_vlen(dt, m[p:p + 16 * n], shape)
         val = np.frombuffer(m, dt, n, p).reshape(shape).copy()
         return name, val
 
     def read_data(self, dt, shape, layout):
+        if isinstance(dt, _VLen):
+            raw = self.read_data(np.dtype("V16"), shape, layout)
+            return self.decode_vlen(dt, np.ascontiguousarray(raw).tobytes(), shape)
         n = int(np.prod(shape)) if shape else 1
         ver = layout[0]
         if ver in (1, 2):
@@ -435,7 +528,11 @@ class _Reader(object):
         attrs = {}
         for mt, body, _ in msgs:
             if mt == 0x000C:
-                k, v = self.attribute(body)
+                try:
+                    k, v = self.attribute(body)
+                except NotImplementedError as e:  # keep loading: callers look attrs up by name
+                    warnings.warn(f"HDF5 attribute skipped: {e}")
+                    continue
                 attrs[k] = v
             elif mt == 0x0015 and struct.unpack_from("<Q", body, 2 + (2 if body[1] & 1 else 0))[0] \
                     != UNDEF:

@@ -210,7 +210,9 @@ def read_model_config(path):
     cfg = root.attrs.get("model_config")
     if cfg is None:
         raise ValueError(f"{path}: no model_config (a weights-only file; use load_weights)")
-    return json.loads(bytes(np.asarray(cfg)).decode("utf8"))
+    if not isinstance(cfg, str):  # fixed-length bytes (Keras' .encode) or a vlen str (h5py str)
+        cfg = bytes(np.asarray(cfg)).decode("utf8")
+    return json.loads(cfg)
 
 
 def load_optimizer_state(model, path):

@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pldepth_amd.dp import GradientAllReducer, shard
+from pldepth_amd.dp import BucketSchedule, allreduce_bucket, shard
 
 
 def _free_port():
@@ -44,17 +44,47 @@ def _spawn(fn, world=2):
     return out
 
 
+def _exchange(flat, offsets, bucket_bytes, group=None):
+    """The trainer's exchange over one simulated backward: the backward reports decreasing
+    'grads[off:] final' offsets; every bucket the schedule releases is all-reduced async."""
+    sched, works, buckets = BucketSchedule(flat.numel(), bucket_bytes), [], []
+    for off in list(offsets) + [0]:
+        b = sched.ready(off)
+        if b is not None:
+            buckets.append(b)
+            works.append(allreduce_bucket(flat, *b, group))
+    for w in works:
+        w.wait()
+    return buckets
+
+
 def _bucketed_sum(rank, world):
     g = torch.arange(1003, dtype=torch.float32) * (rank + 1)
-    GradientAllReducer(g, bucket_bytes=256)()  # 4 buckets of 64 floats... ragged tail
-    return g.numpy()
+    buckets = _exchange(g, [990, 900, 700, 640, 300, 100, 5], bucket_bytes=256)
+    return g.numpy(), buckets
 
 
 def test_bucketed_allreduce_sums_every_element():
     out = _spawn(_bucketed_sum)
     ref = np.arange(1003, dtype=np.float32) * 3
     for r in (0, 1):
-        np.testing.assert_array_equal(out[r], ref)
+        np.testing.assert_array_equal(out[r][0], ref)
+    # >= 64 floats pending releases a bucket; offset 0 always closes the last one
+    assert out[0][1] == [(900, 1003), (700, 900), (300, 700), (100, 300), (5, 100), (0, 5)]
+    assert out[0][1] == out[1][1]
+
+
+def test_bucket_schedule_tiles_the_buffer():
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        n = int(rng.integers(1, 10000))
+        offs = sorted(set(rng.integers(0, n, int(rng.integers(0, 40))).tolist()), reverse=True)
+        s = BucketSchedule(n, bucket_bytes=int(rng.integers(4, 4000)))
+        got = [b for b in (s.ready(o) for o in offs + [0]) if b is not None]
+        assert s.done and got[0][1] == n and got[-1][0] == 0
+        assert all(a[0] == b[1] for a, b in zip(got, got[1:]))  # contiguous, reverse order
+        assert all(lo < hi for lo, hi in got)
+        assert s.ready(0) is None  # nothing left after the last bucket
 
 
 def test_shard_layout():
@@ -68,7 +98,7 @@ def _replica_grads(rank, world):
     its own images), then the all-reduced mean — what every GPU applies in Adam."""
     from tests.test_model_cpu_helpers import shard_grads
     flat = shard_grads(rank, world)
-    GradientAllReducer(flat)()
+    _exchange(flat, [], bucket_bytes=64 << 20)
     flat /= world
     return flat[::97].numpy().copy(), float(flat.sum())  # keep the IPC message small
 

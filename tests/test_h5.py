@@ -181,3 +181,78 @@ def test_model_checkpoint_saves_only_on_improvement(tmp_path):
     for e, v in enumerate([3.0, 2.0, 2.5, 1.0]):
         cb.on_epoch_end(e, {"val_loss": v, "loss": 0.0})
     assert [p.split("/")[-1] for p in _M.saved] == ["m01.h5", "m02.h5", "m04.h5"]
+
+
+def _attr_message(raw, oh_addr, name):
+    """The body of attribute `name` in the version-1 object header at oh_addr."""
+    nmsg, _, size = struct.unpack_from("<HII", raw, oh_addr + 2)
+    q = oh_addr + 16
+    for _ in range(nmsg):
+        mt, ms = struct.unpack_from("<HH", raw, q)
+        body = raw[q + 8:q + 8 + ms]
+        q += 8 + ms
+        if mt == 0x000C:
+            nsz = struct.unpack_from("<H", body, 2)[0]
+            if body[8:8 + nsz].rstrip(b"\0") == name.encode():
+                return body
+    raise KeyError(name)
+
+
+def test_vlen_string_root_attributes_as_h5py_writes_them(tmp_path):
+    """h5py stores a Python str attribute as a variable-length UTF-8 string (class 9,
+    elements in a global-heap collection). A weights file whose root `backend` /
+    `keras_version` and a model file whose `model_config` are vlen strings load through
+    keras_h5 (load_weights, read_model_config). The byte layout checked below is the format
+    specification's (datatype class 9 v1, 'GCOL' v1 collection >= 4 KiB, 16-byte heap ids);
+    no h5py exists here to write a reference file, so parity with h5py output stays unpinned."""
+    src, dst = _cpu_engine(seed=4), _cpu_engine(seed=5)
+    root = hdf5.Group()
+    keras_h5._write_weights(src, root)
+    root.attrs["backend"] = hdf5.VLenStr("tensorflow")
+    root.attrs["keras_version"] = hdf5.VLenStr("2.4.0")
+    path = tmp_path / "vlen.h5"
+    hdf5.save(str(path), root)
+    raw = path.read_bytes()
+    oh = struct.unpack_from("<Q", raw, 64)[0]
+    body = _attr_message(raw, oh, "keras_version")
+    nsz, tsz, ssz = struct.unpack_from("<HHH", body, 2)
+    p = 8 + nsz + (-nsz % 8)
+    dt = body[p:p + tsz]
+    # class 9 v1, string / null-terminated / UTF-8, size 16, base: 1-byte unsigned int
+    assert dt[:8] == bytes([0x19, 0x01, 0x01, 0x00, 16, 0, 0, 0])
+    assert dt[8:20] == bytes([0x10, 0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0])
+    p += tsz + (-tsz % 8) + ssz + (-ssz % 8)
+    ln, coll, idx = struct.unpack_from("<IQI", body, p)
+    assert (ln, idx) == (5, 1) and raw[coll:coll + 4] == b"GCOL" and raw[coll + 4] == 1
+    assert struct.unpack_from("<Q", raw, coll + 8)[0] >= 4096
+    assert raw[coll + 32:coll + 37] == b"2.4.0"
+    r = hdf5.load(str(path))
+    assert r.attrs["keras_version"] == "2.4.0" and r.attrs["backend"] == "tensorflow"
+    assert keras_h5.load_weights(dst, str(path)) == "name"
+    a, b = src.get_weights(), dst.get_weights()
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    # model file: model_config as a vlen str
+    root.attrs["model_config"] = hdf5.VLenStr('{"class_name": "FullyFledgedModel"}')
+    hdf5.save(str(path), root)
+    assert keras_h5.read_model_config(str(path)) == {"class_name": "FullyFledgedModel"}
+
+
+def test_unsupported_attribute_type_is_skipped(tmp_path):
+    """An attribute of a datatype the reader does not decode (here: class 6, compound) is
+    skipped with a warning; the rest of the file still loads."""
+    root = hdf5.Group({"keep": np.int64(3), "odd": np.int64(5)})
+    root.create_dataset("x", np.ones(2, np.float32))
+    path = tmp_path / "u.h5"
+    hdf5.save(str(path), root)
+    raw = bytearray(path.read_bytes())
+    oh = struct.unpack_from("<Q", raw, 64)[0]
+    body = _attr_message(bytes(raw), oh, "odd")
+    at = bytes(raw).index(body)
+    nsz = struct.unpack_from("<H", body, 2)[0]
+    dpos = at + 8 + nsz + (-nsz % 8)
+    raw[dpos] = (1 << 4) | 6  # datatype class -> compound
+    path.write_bytes(bytes(raw))
+    with pytest.warns(UserWarning, match="attribute skipped"):
+        r = hdf5.load(str(path))
+    assert "odd" not in r.attrs and int(r.attrs["keep"]) == 3
+    assert np.array_equal(r["x"].data, [1, 1])

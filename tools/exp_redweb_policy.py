@@ -1,42 +1,72 @@
 """Experiment: ff_redweb at 448x448 batch 32 — forward error vs fp64 per encoder bf16x3
-population threshold, and the eager fwd+bwd time of each."""
+population threshold (i.e. which ResNet stages run exact fp32), next to the torch-CPU fp32
+restatement's own error on the same input, and the eager fwd+bwd time of each (variants: the
+encoder stages kept in exact fp32 under 'auto', RedWebFF.exact_stages).
+Writes gpurun_out/redweb_policy.json."""
+import json
 import os
 import sys
 import time
 
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
+import numpy as np
+import torch
 
 sys.path.insert(0, ".")
 from oracle import redweb as OR  # noqa: E402
-from pldepth_amd import kernels as K  # noqa: E402
 from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input  # noqa: E402
 
 torch.cuda.set_device(0)
-B, H, R, L = 32, 448, 100, 5
+B, H = 32, 448
 rng = np.random.default_rng(32)
 x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
 eng = RedWebFF((H, H, 3), B, seed=0, conv_math="auto")
-P = {k: torch.tensor(v, dtype=torch.float64) for k, v in eng.get_weights().items()}
-taps = {}
+W = eng.get_weights()
+P = {k: torch.tensor(v, dtype=torch.float64) for k, v in W.items()}
+P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in W.items()}
+names = ["conv2_block3_out", "conv3_block4_out", "conv4_block3_out", "conv5_block3_out",
+         "ffl0", "ffl1", "ffl2", "pred"]
+taps, taps32 = {}, {}
 t0 = time.time()
 with torch.no_grad():
-    OR.forward(P, torch.tensor(x, dtype=torch.float64), taps=taps, preprocessed=True)
-print("oracle s", time.time() - t0, flush=True)
-names = ["conv3_block4_out", "conv4_block3_out", "conv5_block3_out", "ffl0", "ffl1"]
+    taps["pred"] = OR.forward(P, torch.tensor(x, dtype=torch.float64), taps=taps,
+                              preprocessed=True)
+    print("oracle fp64 s", time.time() - t0, flush=True)
+    taps32["pred"] = OR.forward(P32, torch.tensor(x), taps=taps32, preprocessed=True)
+print("oracle fp32 s", time.time() - t0, flush=True)
+
+
+def ref_nhwc(t, n):
+    return t if n == "pred" else t.permute(0, 2, 3, 1)
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max())
+
+
+out = {"fp32_restatement": {n: rel(ref_nhwc(taps32[n], n), ref_nhwc(taps[n], n))
+                            for n in names}}
+print("fp32", {k: f"{v:.2e}" for k, v in out["fp32_restatement"].items()}, flush=True)
+del taps32
+
+
+def mine(n):
+    if n == "pred":
+        return eng.act["pred"]
+    return eng.act[n if not n.startswith("ffl") else n + "/out"]
+
+
 dp = torch.randn(B, H, H, 1, device="cuda") * 1e-3
-for thr in [4096, 8192, 16384, 32768, 1 << 40]:
-    eng.x3_min_population = thr
-    eng.set_weights({k: v.float().numpy() for k, v in P.items()})
+VARIANTS = [("bf16x3", ()), ("stem", ("conv1",)), ("stem+conv2", ("conv1", "conv2")),
+            ("conv2", ("conv2",)), ("stem+conv2+conv3", ("conv1", "conv2", "conv3")),
+            ("fp32", ("conv",))]
+for thr, stages in VARIANTS:
+    eng.exact_stages = stages
+    eng.set_weights(W)
     eng.act["input"].copy_(torch.from_numpy(x))
     eng.forward(training=True)
     torch.cuda.synchronize()
-    errs = {}
-    for n in names:
-        mine = eng.act[n if not n.startswith("ffl") else n + "/out"].double().cpu()
-        ref = taps[n].permute(0, 2, 3, 1)
-        errs[n] = float((mine - ref).abs().max() / ref.abs().max())
+    errs = {n: rel(mine(n), ref_nhwc(taps[n], n)) for n in names}
     eng.backward(dp)  # tune
     torch.cuda.synchronize()
     t0 = time.time()
@@ -44,5 +74,9 @@ for thr in [4096, 8192, 16384, 32768, 1 << 40]:
         eng.forward(training=True)
         eng.backward(dp)
     torch.cuda.synchronize()
-    print(thr, f"{(time.time() - t0) / 3 * 1e3:.1f} ms", {k: f"{v:.2e}" for k, v in errs.items()},
-          flush=True)
+    ms = (time.time() - t0) / 3 * 1e3
+    out[str(thr)] = {"ms": ms, "errors": errs}
+    print(thr, f"{ms:.1f} ms", {k: f"{v:.2e}" for k, v in errs.items()}, flush=True)
+os.makedirs("gpurun_out", exist_ok=True)
+with open("gpurun_out/redweb_policy.json", "w") as f:
+    json.dump(out, f, indent=1)
