@@ -14,11 +14,8 @@ import os
 import sys
 import time
 
-# before torch / the HIP runtime initialise: hipGraph replay correctness (pldepth_amd/__init__.py)
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
+import numpy as np
+import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

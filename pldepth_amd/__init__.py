@@ -1,17 +1,1 @@
 """MI355X-native PLDepth training hot path (HIP kernels behind the reference's Python API)."""
-import os
-import sys
-
-# hipGraph replay of the training step must equal eager execution. This ROCm runtime's graph
-# "packet capture" replay path (on by default) does not: replays of the captured step drifted
-# from the eager step after a few iterations (parameters, filter copies, then everything;
-# tools/dbg_graph7.py, tests/test_trainer_gpu.py), while with packet capture off every replay is
-# bit-identical. The flag is read once, when the HIP runtime initialises, so it must be in the
-# environment before the process's first GPU call: the entry points (bench.py, tests/conftest.py,
-# __graft_entry__.py, PLDepth.py) set it before importing torch, and this import sets it when
-# torch is not loaded yet. Graphs are used only when one of those held (GRAPHS_OK); otherwise
-# the trainer steps eagerly — the same kernels and results, more host launch overhead.
-PACKET_CAPTURE_ENV = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
-if PACKET_CAPTURE_ENV not in os.environ and "torch" not in sys.modules:
-    os.environ[PACKET_CAPTURE_ENV] = "0"
-GRAPHS_OK = os.environ.get(PACKET_CAPTURE_ENV) == "0"

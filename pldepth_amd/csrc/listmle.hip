@@ -10,6 +10,8 @@
 // staged in LDS for the O(L) rank computation (lists arrive pre-sorted from the sampler, so the
 // sort is usually the identity; ties keep "later element first", see oracle/listmle.py).
 // HBM-bound: 8 B/element (idx, label) + 4 B gather + 4 B scatter.
+#include <algorithm>
+
 #include "common.h"
 
 namespace pld {
@@ -181,6 +183,21 @@ __global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ x, 
   if (threadIdx.x == 0) out[0] = (float)(red[0] / (double)n);
 }
 
+// dpred = 0 ahead of the scatter. A kernel, not hipMemsetAsync: replayed from a hipGraph with
+// this ROCm runtime's packet capture on, the memset node was not ordered before the scatter
+// kernel that follows it (the atomics landed on a partly cleared buffer and replays drifted;
+// tools/graph_bisect.py isolated this call, tools/graph_memset_repro.hip reproduces it with the
+// runtime alone). Every node of the library's captured steps is now a kernel.
+__global__ __launch_bounds__(256) void zero_kernel(float* __restrict__ p, long n) {
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    p[i] = 0.f;
+}
+
 }  // namespace pld
 
 extern "C" int pld_listmle_fwd_bwd(const float* pred, const float* y_true, int B, int HW, int R,
@@ -192,7 +209,14 @@ extern "C" int pld_listmle_fwd_bwd(const float* pred, const float* y_true, int B
                 "pld_listmle_fwd_bwd: bad shape B=%d HW=%d R=%d L=%d (L must be 1..512)", B, HW,
                 R, L);
   hipStream_t st = as_stream(stream);
-  if (zero_dpred) PLD_HIP(hipMemsetAsync(dpred, 0, sizeof(float) * (size_t)B * HW, st));
+  PLD_CHECK_ARG(!zero_dpred || aligned16(dpred), "pld_listmle_fwd_bwd: dpred must be 16-byte "
+                "aligned");
+  if (zero_dpred) {
+    const long nz = (long)B * HW;
+    zero_kernel<<<(unsigned)std::min<long>(cdiv(nz / 4 + 1, 256), 4096), 256, 0, st>>>(dpred, nz);
+    int rc = check_launch("zero_kernel");
+    if (rc) return rc;
+  }
   const long n = (long)B * R;
   const float inv_n = (float)(1.0 / (double)n);
   dim3 grid(cdiv(n, 4)), block(256);

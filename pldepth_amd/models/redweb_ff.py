@@ -33,6 +33,14 @@ RESNET50_STACKS = [("conv2", 64, 3, 1), ("conv3", 128, 4, 2), ("conv4", 256, 6, 
                    ("conv5", 512, 3, 2)]
 TAPS = ("conv2_block3_out", "conv3_block4_out", "conv4_block3_out", "conv5_block3_out")
 # FeatureFusionLayer(inter, out)([left tap, up]) (redweb.py:426-428)
+# 'auto' conv policy for the frozen ResNet-50: bf16x3 everywhere except the conv2 stage (the
+# 112x112 bottlenecks at 448x448), which runs exact fp32. The random-init ResNet-50 under
+# training-mode BN amplifies a perturbation ~100x from conv2_block3_out to conv5_block3_out:
+# bf16x3 rounding entering in the conv2 stage alone puts conv5_block3_out 1.2e-3 from fp64
+# (batch 32, 448x448), with that stage exact it is at the fp32 restatement's own 5e-4;
+# exact stem / conv3-5 stages change nothing measurable. Cost: +1.8 ms per fwd+bwd
+# (36.9 -> 38.7 ms eager; tools/exp_redweb_policy.py, profiles/r03_redweb_policy.txt).
+EXACT_STAGES_AUTO = ("conv2",)
 FFLS = [("ffl0", 256, 256, "conv4_block3_out"),
         ("ffl1", 128, 128, "conv3_block4_out"),
         ("ffl2", 64, 64, "conv2_block3_out")]
@@ -69,7 +77,7 @@ class RedWebFF:
         self._alloc()
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
-        self.exact_stages = ()
+        self.exact_stages = EXACT_STAGES_AUTO
         self.seed = seed
 
     preprocess = staticmethod(preprocess_input)

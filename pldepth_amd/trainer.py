@@ -273,15 +273,7 @@ class ReplicaTrainer:
             self._update()
 
     def capture(self):
-        """Capture the step into hipGraph(s). Call after one eager step (workspaces sized).
-        A no-op (the step stays eager) when graph replay is not known to be exact in this
-        process (pldepth_amd.GRAPHS_OK: HIP initialised before packet capture could be off)."""
-        from . import GRAPHS_OK
-        if not GRAPHS_OK:
-            import warnings
-            warnings.warn("hipGraph capture skipped: set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before "
-                          "the first GPU call (see pldepth_amd/__init__.py); stepping eagerly")
-            return
+        """Capture the step into hipGraph(s). Call after one eager step (workspaces sized)."""
         if self.world > 1:
             self._capture_dp()
             return

@@ -1,10 +1,7 @@
 import os
 import sys
 
-# before torch / the HIP runtime initialise: hipGraph replay correctness (pldepth_amd/__init__.py)
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
-import pytest  # noqa: E402
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

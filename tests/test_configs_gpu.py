@@ -362,11 +362,32 @@ def test_sampler_empty_mask_is_defined(cuda):
 
 
 # ------------------------------------------------- the bench's arithmetic at its own batch
+def _oracle_step(O, P, x, y, B, L, taps=None, **kw):
+    """One oracle forward (taps recorded) + hourglass ListMLE + backward: (pred, loss, dpred,
+    grads of the trainable tensors). dpred is taken from this forward's own prediction."""
+    names = set(O.trainable_names(P))
+    Q = {k: (v.detach().clone().requires_grad_(True) if k in names else v.detach())
+         for k, v in P.items()}
+    out = O.forward(Q, x, taps=taps, **kw)
+    loss, dpred = LM.hourglass_nll(y, out.detach().double().numpy(), B, L)
+    out.backward(torch.tensor(dpred, dtype=out.dtype))
+    if taps is not None:
+        for k in list(taps):
+            taps[k] = taps[k].detach()
+    grads = {k: Q[k].grad.detach() for k in names}
+    return out.detach(), loss, dpred, grads
+
+
+@pytest.mark.timeout(1500)
 @pytest.mark.parametrize("model", ["ff_effnet", "ff_redweb"])
-def test_forward_batch32_bench_policy(cuda, model):
-    """cfg2 / cfg3 forward exactly as the bench runs it: 448x448, batch 32, the default 'auto'
-    conv policy (bf16x3 wherever a BN normalises over >= 4096 values per channel — at batch 32
-    every conv). Taps, prediction and loss within 1e-3 of the fp64 oracle."""
+def test_batch32_bench_policy(cuda, model):
+    """cfg2 / cfg3 exactly as the bench runs them: 448x448, batch 32, the default 'auto' conv
+    policy (ff_effnet: bf16x3 everywhere; ff_redweb: bf16x3 except the stem and conv2 stage,
+    RedWebFF.exact_stages). Forward taps, prediction, loss and every trainable gradient against
+    the fp64 oracle, next to the torch-CPU fp32 restatement of the same reference semantics on
+    the same input: every tap and the prediction within max(1e-3, 2x the fp32 restatement's
+    error), the loss within 1e-3, the gradients by check_gradients' bar (1e-3 wherever the
+    fp32 restatement meets it). Reports go to $PLD_REPORT_DIR."""
     B, H, R, L = 32, 448, 100, 5
     rng = np.random.default_rng(32)
     x = rng.random((B, H, H, 3)).astype(np.float32)
@@ -377,44 +398,53 @@ def test_forward_batch32_bench_policy(cuda, model):
         names = ["stem_activation", "block2a_output", "block3a_expand_activation",
                  "block5c_output", "block7a_output", "top_activation"]
         mine = eng.tap
+        zero = effnet_structural_zero
     else:
         from pldepth_amd.models.redweb_ff import RedWebFF, preprocess_input
         eng = RedWebFF((H, H, 3), B, seed=0, conv_math="auto")
         x = preprocess_input(x)
         O, kw = OR, {"preprocessed": True}
         names = ["conv1_relu", "conv2_block3_out", "conv3_block4_out", "conv4_block3_out",
-                 "conv5_block3_out", "ffl0", "ffl1"]
+                 "conv5_block3_out", "ffl0", "ffl1", "ffl2"]
         mine = lambda n: eng.act[n if not n.startswith("ffl") else n + "/out"]
+        zeros = {"aol/conv0/bias", "aol/conv1/bias", "aol/conv2/bias"}
+        zero = lambda k: k in zeros
     assert eng.enc_math == "auto"
     weights = eng.get_weights()
     eng.act["input"].copy_(torch.from_numpy(x))
     pred = eng.forward(training=True)
     y = make_rankings(rng, B, H, H, R, L)
-    loss, _, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
+    loss, dpred, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
+    eng.backward(dpred)
     torch.cuda.synchronize()
+    hip_taps = {n: mine(n).detach().cpu().double() for n in names}
+    hip_pred, hip_loss = pred.detach().cpu().double(), loss.item()
+    hip_grads = {k: eng.grads[k].detach().cpu() for k in O.trainable_names(weights)}
+    del eng, pred, dpred
+    torch.cuda.empty_cache()
     P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
     taps = {}
+    pred_ref, loss_ref, dpred_ref, g64 = _oracle_step(
+        O, P, torch.tensor(x, dtype=torch.float64), y, B, L, taps=taps, **kw)
+    ref = {n: taps[n].permute(0, 2, 3, 1) for n in names}
+    del taps
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    taps32 = {}
     with torch.no_grad():
-        pred_ref = O.forward(P, torch.tensor(x, dtype=torch.float64), taps=taps, **kw)
-    errs = {n: rel(mine(n), taps[n].permute(0, 2, 3, 1)) for n in names}
-    errs["pred"] = rel(pred, pred_ref)
-    loss_ref, _ = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
-    errs["loss"] = abs(loss.item() - loss_ref) / abs(loss_ref)
-    bars = {n: TOL for n in errs}
-    if model == "ff_redweb":
-        # ResNet-50 amplifies rounding ~3x per stage at this (random) initialisation: the same
-        # forward with an exact-fp32 encoder ('mixed') lands ~5e-4 from fp64 at conv5 already,
-        # bf16x3 1.2e-3 (autotuned schedules) to 1.34e-3 (the built-in ones, split-K order
-        # differs). Bar: 1e-3, or 3x what exact fp32 reaches on the same input.
-        ref_eng = RedWebFF((H, H, 3), B, seed=0, conv_math="mixed")
-        ref_eng.act["input"].copy_(torch.from_numpy(x))
-        ref_pred = ref_eng.forward(training=True)
-        torch.cuda.synchronize()
-        for n in names:
-            t = ref_eng.act[n if not n.startswith("ffl") else n + "/out"]
-            bars[n] = max(TOL, 3.0 * rel(t, taps[n].permute(0, 2, 3, 1)))
-        bars["pred"] = max(TOL, 3.0 * rel(ref_pred, pred_ref))
-        del ref_eng
-    report(f"{model}_b32_forward", {"errors": errs, "bars": bars})
+        pred32 = O.forward(P32, torch.tensor(x), taps=taps32, **kw)
+    e32 = {n: rel(taps32[n].permute(0, 2, 3, 1), ref[n]) for n in names}
+    e32["pred"] = rel(pred32, pred_ref)
+    del taps32, pred32
+    g32 = O.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(), **kw)[0]
+    errs = {n: rel(hip_taps[n], ref[n]) for n in names}
+    errs["pred"] = rel(hip_pred, pred_ref)
+    errs["loss"] = abs(hip_loss - loss_ref) / abs(loss_ref)
+    bars = {n: max(TOL, 2.0 * e32[n]) for n in e32}
+    bars["loss"] = TOL
+    report(f"{model}_b32_auto_forward", {"errors": errs, "bars": bars, "fp32_restatement": e32})
     print(errs, bars)
     assert all(errs[n] < bars[n] for n in errs), (errs, bars)
+    glob = check_gradients(f"{model}_b32_auto_grads", hip_grads, g64, g32, zero)
+    # at the bench's batch the BN reductions span 16x the values of the batch-2 tests: the
+    # 1e-3 branch of the bar governs most tensors
+    assert glob["tensors_fp32_within_1e-3"] >= glob["tensors"] // 2, glob

@@ -1,14 +1,15 @@
 """The graph-replayed training step equals the eager one, step after step (the bench times the
 replay; tests/test_configs_gpu.py checks the eager step against the oracle).
 
-Regression test for a ROCm runtime behaviour: with hipGraph packet capture on (the runtime's
-default), replays drifted from eager execution within a few steps; pldepth_amd/__init__.py turns
-it off before HIP initialises."""
+Regression test for the replay drift of round 2: with this ROCm runtime's graph packet capture
+(its default) a captured hipMemsetAsync was not ordered before the kernel after it, so the
+ListMLE scatter-add landed on a partly cleared gradient buffer (tools/graph_bisect.py isolated
+pld_listmle_fwd_bwd; tools/graph_memset_repro.hip reproduces it with the runtime alone). The
+library no longer records memset nodes; the test runs with the runtime's default settings."""
 import numpy as np
 import pytest
 import torch
 
-import pldepth_amd
 from pldepth_amd.trainer import ReplicaTrainer
 
 pytestmark = pytest.mark.gpu
@@ -30,7 +31,6 @@ def _state(t):
 
 @pytest.mark.parametrize("model", ["ff_effnet", "ff_redweb"])
 def test_graph_replay_equals_eager(cuda, model):
-    assert pldepth_amd.GRAPHS_OK
     B, H, L, R = 2, 64, 5, 20
     rng = np.random.default_rng(0)
     x = torch.from_numpy(rng.random((B, H, H, 3)).astype(np.float32)).to(cuda)
