@@ -121,15 +121,116 @@ def profile_conv(trainer, lr):
     for n, m in (("upconv_fwd", 0), ("upconv_dgrad", 1), ("upconv_wgrad", 2),
                  ("upconv_bwd", 1)):
         setattr(K, n, up_wrap(n, m))
+    # one stream: each kernel's events bracket it alone (the engine's decoder weight gradients
+    # otherwise overlap the rest of the backward on a side stream)
+    overlap = getattr(trainer.engine, "overlap_wgrad", False)
+    trainer.engine.overlap_wgrad = False
     try:
         trainer.step_eager(lr)
         st.synchronize()
     finally:
+        trainer.engine.overlap_wgrad = overlap
         for n, f in orig.items():
             setattr(K, n, f)
         for n, f in up_orig.items():
             setattr(K, n, f)
     return [(n, k, m, f, b, e0.elapsed_time(e1) / 1e3) for n, k, m, f, b, e0, e1 in recs]
+
+
+# kernels.py wrapper -> op family (the step-level byte floor and the PMC traffic per family)
+def _family(fn):
+    if fn.startswith(("conv2d", "pgemm", "upconv", "channel_sum", "filter_split")):
+        return "conv"
+    if fn.startswith(("bn_", "channel_affine")):
+        return "batchnorm"
+    if fn.startswith("dwconv"):
+        return "depthwise"
+    if fn.startswith("se_"):
+        return "squeeze_excite"
+    if fn.startswith(("upsample", "maxpool", "residual", "scale_per_sample", "dropconnect")):
+        return "resample_residual"
+    if fn.startswith(("sampler", "listmle")):
+        return "sampler_listmle"
+    return "optimizer_refresh"  # adam, filter_refresh, step / scalar updates
+
+
+def step_byte_floor(trainer, lr):
+    """Step-level algorithmic byte floor: one eager step with every kernels.py entry point
+    wrapped; each call counts every distinct tensor it is handed ONCE (its inputs read once, its
+    outputs written once; a tensor it reads and writes in place counts once; library scratch
+    workspaces not at all). Summed per op family = "each activation written once and read once
+    per consumer" for the launch sequence this build runs. Returns {family: bytes}, total."""
+    from pldepth_amd import kernels as K
+    ws_ptrs = lambda: {b.data_ptr() for b in K._ws_cache.values()}
+    depth, seen, fam = [0], [None], {}
+    orig_ptr = K.ptr
+
+    def ptr(t):
+        if t is not None and depth[0] > 0 and seen[0] is not None:
+            seen[0][t.data_ptr()] = t.numel() * t.element_size()
+        return orig_ptr(t)
+
+    names = [n for n, f in vars(K).items() if callable(f) and not n.startswith("_")
+             and getattr(f, "__module__", None) == K.__name__ and n not in (
+                 "ptr", "stream", "workspace", "conv_args", "conv_policy", "encoder_math",
+                 "set_conv_math", "same_pads", "sampler_candidates", "pgemm_ok", "pgemm_pays",
+                 "load_tile_cache", "save_tile_cache", "Graph")]
+    saved = {n: getattr(K, n) for n in names}
+
+    def wrap(n, f):
+        def w(*args, **kw):
+            outer = depth[0] == 0
+            if outer:
+                seen[0] = {}
+            depth[0] += 1
+            try:
+                for a in list(args) + list(kw.values()):
+                    keep = getattr(a, "_keep", None)  # ConvArgs: x1, x2, in_scale, in_shift
+                    if keep is not None:
+                        for t in keep:
+                            if t is not None:
+                                seen[0][t.data_ptr()] = t.numel() * t.element_size()
+                return f(*args, **kw)
+            finally:
+                depth[0] -= 1
+                if outer:
+                    skip = ws_ptrs()
+                    fam[_family(n)] = fam.get(_family(n), 0) + sum(
+                        v for p, v in seen[0].items() if p not in skip)
+                    seen[0] = None
+        return w
+
+    K.ptr = ptr
+    for n in names:
+        setattr(K, n, wrap(n, saved[n]))
+    try:
+        trainer.step_eager(lr)
+        trainer.synchronize()
+    finally:
+        K.ptr = orig_ptr
+        for n, f in saved.items():
+            setattr(K, n, f)
+    return fam, sum(fam.values())
+
+
+def attach_step_traffic(roof, path, workload):
+    """The measured side of the byte floor: per-family HBM bytes of one eager step from the
+    committed PMC profile (tools/pmc_step_family.py), only when its workload matches."""
+    if path and not os.path.isabs(path):
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), path)
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return
+    if t.get("workload") != workload:
+        return
+    alg = roof["step_bytes_algorithmic"]
+    roof["step_bytes_measured"] = {
+        "total": t["total_bytes"], "by_family": t["by_family"], "profile": path,
+        "over_algorithmic": round(t["total_bytes"] / alg["total"], 3),
+        "note": "PMC FETCH_SIZE x2 (gfx950 64-B tally) + WRITE_SIZE of one eager step; FETCH "
+                "counts Infinity-Cache hits too, so these are upper bounds on HBM bytes"}
 
 
 def attach_traffic(roof, path, workload):
@@ -427,6 +528,9 @@ def main():
                     help="PMC traffic of the dominant kernel (tools/dominant_traffic.py, committed "
                          "from the same HEAD and workload): fills roofline.traffic when its kernel "
                          "and workload match this run's")
+    ap.add_argument("--step-traffic-profile", default="profiles/r03_pmc_step_family.json",
+                    help="PMC HBM bytes of one eager step per op family "
+                         "(tools/pmc_step_family.py): roofline.step_bytes_measured")
     ap.add_argument("--tile-cache", default="",
                     help="JSON of tuned conv schedules: loaded if present, written after tuning")
     a = ap.parse_args()
@@ -473,6 +577,12 @@ def main():
                 f"rankings_per_image {R}, sampler {tr.strategy}, Adam-AMSGrad")
     attach_traffic(roof, a.traffic_profile, workload)
     roof["step_frac"] = round(value / world * flops_img / 1e12 / roof["family"]["peak"], 4)
+    fam, total = step_byte_floor(tr, 0.01)
+    roof["step_bytes_algorithmic"] = {
+        "total": total, "by_family": dict(sorted(fam.items(), key=lambda kv: -kv[1])),
+        "definition": "per launch, every distinct tensor the call is handed counted once (inputs "
+                      "read once, outputs written once), summed over one step's launches"}
+    attach_step_traffic(roof, a.step_traffic_profile, workload)
     out = {
         "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
         "value": round(value, 3),

@@ -5,10 +5,11 @@ The reference trains on one device; the build shards HR-WSI-shape
 rank r owns images [r*B, (r+1)*B) of the global batch (contiguous), draws its rankings and
 drop-connect masks from Philox counters keyed by the GLOBAL image index (so results do not
 depend on the GPU count), keeps BN statistics per replica (TF MirroredStrategy semantics) and
-exchanges exactly one thing per step: the fp32 gradient, summed by all-reduce in reverse-order
-buckets as the backward finalises them (``BucketSchedule``) and averaged inside the Adam kernel
-(grad_scale = 1/world). ``ReplicaTrainer`` (trainer.py) drives both, eagerly and between the
-segment graphs of its captured step.
+exchanges exactly one thing per step: the fp32 gradient, summed by all-reduce in reverse-order,
+tensor-aligned buckets (``tensor_buckets``) and averaged inside the Adam kernel (grad_scale =
+1/world). ``ReplicaTrainer`` (trainer.py) issues them after its (graph-replayed) backward, each
+bucket's Adam-AMSGrad + filter refresh running on a side stream as soon as that bucket lands,
+i.e. the exchange overlaps the optimizer step.
 """
 import os
 
@@ -26,34 +27,26 @@ def shard(global_batch, rank, world):
     return rank * per, per
 
 
-class BucketSchedule(object):
-    """Bucket boundaries of a flat gradient buffer that the backward finalises from the end
-    towards offset 0 (engine.backward(grad_ready=...) reports 'grads[off:] are final').
+def tensor_buckets(offsets, numel, bucket_bytes=8 << 20, elem_bytes=4):
+    """Reverse-order buckets of a flat gradient buffer, aligned to tensor starts.
 
-    ready(off) returns the bucket (lo, hi) to exchange now — once at least `bucket_bytes` are
-    pending, and always at off == 0 (the end of the backward) — or None. Over one backward the
-    buckets tile [0, numel) exactly, in reverse order. ~8 MB buckets: large enough that each
-    RCCL ring all-reduce runs at link rate over xGMI (7 x ~153 GB/s point-to-point links), small
-    enough that the first one starts while most of the backward is still running."""
-
-    def __init__(self, numel, bucket_bytes=8 << 20, elem_bytes=4):
-        self.numel, self.bucket_bytes, self.elem_bytes = int(numel), int(bucket_bytes), elem_bytes
-        self.reset()
-
-    def reset(self):
-        self.hi = self.numel
-
-    def ready(self, off):
-        pending = (self.hi - off) * self.elem_bytes
-        if off < self.hi and (pending >= self.bucket_bytes or off == 0):
-            bucket = (int(off), self.hi)
-            self.hi = int(off)
-            return bucket
-        return None
-
-    @property
-    def done(self):
-        return self.hi == 0
+    offsets: flat start offsets of the parameter tensors (any order). Tensors are grouped from
+    the end of the buffer towards offset 0 (the order the backward finalises them) into buckets
+    of at least `bucket_bytes` (the last one, at offset 0, may be smaller; a tensor larger than
+    a bucket is a bucket of its own). No tensor spans two buckets, so a bucket's optimizer
+    update can refresh the derived copies (native conv filters) of every tensor in it. The
+    buckets tile [0, numel) exactly. ~8 MB: large enough that each RCCL ring all-reduce runs at
+    link rate over xGMI (7 x ~153 GB/s point-to-point links), small enough that the updates of
+    the first buckets overlap the all-reduces of the later ones."""
+    starts = sorted(set(int(o) for o in offsets) | {0})
+    if starts[-1] >= numel:
+        raise ValueError("tensor offset beyond the buffer")
+    buckets, hi = [], int(numel)
+    for lo in reversed(starts):
+        if (hi - lo) * elem_bytes >= bucket_bytes or lo == 0:
+            buckets.append((lo, hi))
+            hi = lo
+    return buckets
 
 
 def allreduce_bucket(flat, lo, hi, group=None):
@@ -63,4 +56,4 @@ def allreduce_bucket(flat, lo, hi, group=None):
     return dist.all_reduce(flat[lo:hi], group=group, async_op=True)
 
 
-__all__ = ["env_rank_world", "shard", "BucketSchedule", "allreduce_bucket"]
+__all__ = ["env_rank_world", "shard", "tensor_buckets", "allreduce_bucket"]

@@ -488,8 +488,10 @@ def conv2d_wgrad(args, dy, dw, accumulate=False):
     _end(args, tile_in)
 
 
-def channel_sum(x, rows, c, out, accumulate=False):
-    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+def channel_sum(x, rows, c, out, accumulate=False, ws_key="reduce"):
+    """out[c] (+)= sum over rows of x[rows, c]; ws_key: the workspace to use (a call on another
+    stream than the BN reductions needs its own)."""
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), ws_key)
     lib().pld_channel_sum(ptr(x), rows, c, ptr(out), int(accumulate), ptr(ws), stream())
 
 

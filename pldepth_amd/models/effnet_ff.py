@@ -124,6 +124,12 @@ class EffNetFF:
         # training: the last decoder stage's upsample runs inside the final conv's kernels
         # (csrc/upconv.hip); False = the unfused upsample2x + 3x3 conv path
         self.fuse_final = True
+        # backward: the decoder convs' weight gradients (dW + bias sums) on a side stream, joined
+        # at the end of the backward: 1 = each forked once its layer's pre-BN gradient exists
+        # (concurrent with the rest of the decoder chain), 2 = all forked after the last decoder
+        # dgrad (concurrent with the encoder backward, which has no weight gradients of its
+        # own); 0 = in line
+        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "0"))
 
     # ------------------------------------------------------------------ graph structure
     def _build_spec(self):
@@ -316,11 +322,18 @@ class EffNetFF:
             self._k12[c] = torch.empty(2 * c, device=self.device)
         return self._k12[c]
 
-    def _gpre_buf(self, shape):
-        key = tuple(shape)
+    def _gpre_buf(self, shape, slot=0):
+        key = (tuple(shape), slot)
         if key not in self._gpre:
-            self._gpre[key] = torch.empty(key, device=self.device)
+            self._gpre[key] = torch.empty(key[0], device=self.device)
         return self._gpre[key]
+
+    def _wgrad_side(self):
+        """(stream, fork events) of the decoder's weight-gradient side stream (created once)."""
+        if not hasattr(self, "_wside"):
+            self._wside = (torch.cuda.Stream(device=self.device),
+                           [torch.cuda.Event() for _ in range(len(self.dec) + 1)])
+        return self._wside
 
     # ------------------------------------------------------------------ forward
     def _em(self, oh, ow):
@@ -506,6 +519,13 @@ class EffNetFF:
         a = K.conv_args
         h, w = self.H, self.W
         ready = grad_ready or (lambda off: None)
+        # the side stream needs its own buffers: gradients it reads are never recycled by the
+        # main stream's later layers (slot "dec"), its bias sums use their own workspace
+        side = bool(self.overlap_wgrad) and grad_ready is None
+        main = torch.cuda.current_stream(self.device)
+        if side:
+            wstream, fork = self._wgrad_side()
+            deferred = []
         # final conv (bias, no BN)
         last = len(self.dec) - 1
         if self.fuse_final:
@@ -513,7 +533,7 @@ class EffNetFF:
             # dec4's activation gradient and the whole dec_bn4 + ReLU backward (its channel
             # reductions accumulated in the same pass) into dec4's pre-BN gradient
             _, bn4, _ = self.dec[last]
-            gpre4 = self._gpre_buf(A[f"dec{last}_pre"].shape)
+            gpre4 = self._gpre_buf(A[f"dec{last}_pre"].shape, "dec" if side else 0)
             K.upconv_bwd(A["dec4_pre"], (bn4.mean, bn4.invstd, bn4.gamma, bn4.beta),
                          self.final.w_nat, dpred, G[f"dec{last}_act"], dw=self.final.dw,
                          dx=gpre4, dgamma=bn4.dgamma, dbeta=bn4.dbeta)
@@ -535,7 +555,7 @@ class EffNetFF:
             if not (i == last and self.fuse_final):
                 K.upsample2x_bwd(G[f"dec{i}_up"], G[f"dec{i}_act"])
             rows = B * h * w
-            gpre = self._gpre_buf(A[f"dec{i}_pre"].shape)
+            gpre = self._gpre_buf(A[f"dec{i}_pre"].shape, "dec" if side else 0)
             if not (i == last and self.fuse_final):  # (fused: done by upconv_bwd above)
                 bn.bwd(A[f"dec{i}_pre"], G[f"dec{i}_act"], rows, "relu", gpre)
             if i == 0:
@@ -548,10 +568,28 @@ class EffNetFF:
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
             args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
-            K.conv2d_wgrad(args, gpre, conv.dw)
-            K.channel_sum(gpre, rows, conv.cout, conv.db)
+            if side:
+                def wg(args=args, gpre=gpre, rows=rows, conv=conv):
+                    K.conv2d_wgrad(args, gpre, conv.dw)
+                    K.channel_sum(gpre, rows, conv.cout, conv.db, ws_key="reduce_side")
+                if self.overlap_wgrad == 2:
+                    deferred.append(wg)
+                else:
+                    fork[i].record(main)
+                    with torch.cuda.stream(wstream):
+                        wstream.wait_event(fork[i])
+                        wg()
+            else:
+                K.conv2d_wgrad(args, gpre, conv.dw)
+                K.channel_sum(gpre, rows, conv.cout, conv.db)
             K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
             ready(self.param_offset(f"dec_conv{i}/kernel"))
+        if side and deferred:
+            fork[-1].record(main)
+            with torch.cuda.stream(wstream):
+                wstream.wait_event(fork[-1])
+                for wg in deferred:
+                    wg()
         # encoder
         h, w = A["top_pre"].shape[1:3]
         rows = B * h * w
@@ -567,6 +605,8 @@ class EffNetFF:
             self._block_bwd(blk, x_in, gx_in)
         rows = B * A["stem_pre"].shape[1] * A["stem_pre"].shape[2]
         self.stem_bn.bwd(A["stem_pre"], G["stem_activation"], rows, "swish", None)
+        if side:  # join: every weight gradient is final on the caller's stream from here
+            main.wait_stream(wstream)
         ready(0)
 
     def _block_bwd(self, blk, x_in, gx_in):

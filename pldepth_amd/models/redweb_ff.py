@@ -20,6 +20,7 @@ it), each post-activation tensor a later op reads, and one gradient buffer per a
 The encoder convs need dX only (frozen), the stem conv neither dX nor dW.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -78,6 +79,9 @@ class RedWebFF:
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
+        # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
+        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "0"))
+        self._side = False
         self.seed = seed
 
     preprocess = staticmethod(preprocess_input)
@@ -349,16 +353,39 @@ class RedWebFF:
         return A[n + "/out"]
 
     # ------------------------------------------------------------------ backward
+    def _wslot(self, conv, slot=0):
+        """Buffer slot of a trainable conv's output gradient: its own while the side stream may
+        still read it (weight-gradient overlap), else the shared per-shape slot."""
+        return ("w", conv.name) if self._side else slot
+
+    def _wgrad_side(self):
+        """(stream, per-conv fork events) of the decoder's weight-gradient side stream."""
+        if not hasattr(self, "_wside"):
+            self._wside = (torch.cuda.Stream(device=self.device),
+                           {c.name: torch.cuda.Event() for c in self.convs if c.trainable})
+        return self._wside
+
     def _wgrad_dgrad(self, conv, x, gy, h, w, oh, ow, gx, gx_acc=False):
-        """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given."""
+        """dW (+db) for trainable convs, dX (=|+=) into gx when gx is given. With the weight-
+        gradient overlap, dW and db run on the side stream, forked here (gy complete)."""
         k, s = conv.k, conv.stride
         pt = pl = ((k - 1) // 2 if s == 1 else 0)
         args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout,
                            math=self._math(conv, oh, ow))
         if conv.trainable:
-            K.conv2d_wgrad(args, gy, conv.dw)
-            if conv.db is not None:
-                K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db)
+            if self._side:
+                wstream, fork = self._wgrad_side()
+                fork[conv.name].record(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(wstream):
+                    wstream.wait_event(fork[conv.name])
+                    K.conv2d_wgrad(args, gy, conv.dw)
+                    if conv.db is not None:
+                        K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db,
+                                      ws_key="reduce_side")
+            else:
+                K.conv2d_wgrad(args, gy, conv.dw)
+                if conv.db is not None:
+                    K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db)
         if gx is not None:
             K.conv2d_dgrad(args, gy, conv.w_dg, gx, None, acc1=gx_acc)
 
@@ -371,13 +398,17 @@ class RedWebFF:
         tail of the flat buffer, from its first trainable conv on) are final, and at the end."""
         A, G, B = self.act, self.gact, self.B
         ready = grad_ready or (lambda off: None)
+        # decoder weight gradients on a side stream (EffNetFF.backward); a data-parallel caller
+        # (grad_ready) keeps the single-stream order
+        self._side = bool(self.overlap_wgrad) and grad_ready is None
+        main = torch.cuda.current_stream(self.device)
         H, W = self.H, self.W
         h, w = H // 2, W // 2
         # AdaptiveOutputLayer
         self._wgrad_dgrad(self.aol2, A["aol/up"], dpred, H, W, H, W, G["aol/up"])
         K.upsample2x_bwd(G["aol/up"], G["aol/pre1"])
         self._wgrad_dgrad(self.aol1, A["aol/act0"], G["aol/pre1"], h, w, h, w, G["aol/act0"])
-        g0 = self._gpre_buf(A["aol/pre0"].shape)
+        g0 = self._gpre_buf(A["aol/pre0"].shape, self._wslot(self.aol0))
         self.aol_bn.bwd(A["aol/pre0"], G["aol/act0"], B * h * w, "relu", g0)
         self._wgrad_dgrad(self.aol0, A["ffl2/out"], g0, h, w, h, w, G["ffl2/out"])
         # feature fusion layers, top (ffl2) to bottom (ffl0)
@@ -400,6 +431,9 @@ class RedWebFF:
         hp, wp = A["pool1_pool"].shape[1:3]
         K.maxpool2d_bwd(G["pool1_pool"], self.pool_argmax, 3, 2, 1, 1, G["conv1_relu"])
         self.stem_bn.bwd(A["conv1_pre"], G["conv1_relu"], B * h * w, "relu", None)
+        if self._side:  # join: every weight gradient is final on the caller's stream
+            main.wait_stream(self._wgrad_side()[0])
+        self._side = False
         ready(0)
 
     def _block_bwd(self, blk, x, gx, gx_is_tap):
@@ -434,15 +468,15 @@ class RedWebFF:
         for half in (3, 0):
             xin = x if half == 0 else A[f"{n}/out0"]
             gin = gx if half == 0 else G[f"{n}/out0"]
-            gp = self._gpre_buf(A[f"{n}/pre{half + 2}"].shape)
+            gp = self._gpre_buf(A[f"{n}/pre{half + 2}"].shape, self._wslot(c[half + 2]))
             b[half + 2].add_bwd(A[f"{n}/pre{half + 2}"], gy, rows, xin, "relu", gp, gin)
             self._wgrad_dgrad(c[half + 2], A[f"{n}/act{half + 1}"], gp, h, w, h, w,
                               G[f"{n}/act{half + 1}"])
-            gq = self._gpre_buf(A[f"{n}/pre{half + 1}"].shape)
+            gq = self._gpre_buf(A[f"{n}/pre{half + 1}"].shape, self._wslot(c[half + 1]))
             b[half + 1].bwd(A[f"{n}/pre{half + 1}"], G[f"{n}/act{half + 1}"], rows, "relu", gq)
             self._wgrad_dgrad(c[half + 1], A[f"{n}/act{half}"], gq, h, w, h, w,
                               G[f"{n}/act{half}"])
-            gq0 = self._gpre_buf(A[f"{n}/pre{half}"].shape, 1)
+            gq0 = self._gpre_buf(A[f"{n}/pre{half}"].shape, self._wslot(c[half], 1))
             b[half].bwd(A[f"{n}/pre{half}"], G[f"{n}/act{half}"], rows, "relu", gq0)
             self._wgrad_dgrad(c[half], xin, gq0, h, w, h, w, gin, gx_acc=True)
             gy = gin
@@ -455,13 +489,13 @@ class RedWebFF:
         K.upsample2x_bwd(G[n + "/out"], gd)
         # block_down: input gradient lands in G[sum]; sum = bn1(up_pre) + block_left output
         self._bottleneck_bwd(d["down"], A[n + "/sum"], G[n + "/sum"], gd, h, w)
-        gu = self._gpre_buf(A[n + "/up_pre"].shape)
+        gu = self._gpre_buf(A[n + "/up_pre"].shape, self._wslot(d["conv1"]))
         d["bn1"].bwd(A[n + "/up_pre"], G[n + "/sum"], rows, "none", gu)
         self._wgrad_dgrad(d["conv1"], up, gu, h, w, h, w, gup)
         # block_left receives G[sum] unchanged (identity branch of the add)
         self._bottleneck_bwd(d["left"], A[n + "/left_bn"], G[n + "/left_bn"], G[n + "/sum"],
                              h, w)
-        gl = self._gpre_buf(A[n + "/left_pre"].shape)
+        gl = self._gpre_buf(A[n + "/left_pre"].shape, self._wslot(d["conv0"]))
         d["bn0"].bwd(A[n + "/left_pre"], G[n + "/left_bn"], rows, "none", gl)
         self._wgrad_dgrad(d["conv0"], left, gl, h, w, h, w, gleft)
 

@@ -8,21 +8,18 @@ all-reduce the reference never had: one process per GPU, torch.di
 "nccl" backend (= RCCL over xGMI), per-rank batch B, BN statistics per replica (MirroredStrategy
 semantics), one fp32 all-reduce of the flat gradient buffer, 1/world folded into Adam.
 
-Stepping: the whole step is stream-ordered HIP work with no host synchronisation. N = 1: one
-hipGraph per step (captured after a first eager step). N > 1: the gradient exchange overlaps the
-backward: the backward reports, layer by layer, which tail of the flat gradient buffer is final
-(engine.backward(grad_ready=...)); each ~8 MB bucket is all-reduced asynchronously as it
-completes (RCCL on its own stream) and a side stream runs that bucket's Adam-AMSGrad + filter
-refresh as soon as it lands, while the compute stream carries on with the rest of the backward
-(the decoder holds 99.6 % of the gradient bytes and finishes before the encoder backward
-starts). The N > 1 step is captured too, in segments: the compute stream's work between two
-bucket boundaries is one hipGraph, each bucket's update another (on the side stream); a replay
-launches the segment graphs and, between them, issues the bucket all-reduces through
-torch.distributed (the collectives stay outside the graphs: RCCL's own stream, c10d's stream
-dependencies and its work objects run as they do eagerly). Per step the host then issues
-~2 graph launches + 1 collective per bucket instead of ~500 kernel launches. Per-step scalars
-(learning rate, step counter) live in device memory.
+Stepping: the whole step is stream-ordered HIP work with no host synchronisation, replayed from
+hipGraphs captured after a first eager step. Inside the backward the decoder's weight gradients
+run on a side stream concurrently with the rest of the chain (engine.overlap_wgrad). N = 1: one
+graph per step. N > 1: the compute (sampler -> forward -> ListMLE -> backward) is one graph;
+then the gradient is all-reduced in ~8 MB tensor-aligned buckets in reverse layer order (RCCL on
+its own stream, issued through torch.distributed between graph launches), and a side stream runs
+each bucket's Adam-AMSGrad + filter refresh (one captured graph per bucket) as soon as it lands —
+the exchange overlaps the optimizer step. Per-step scalars (learning rate, step counter) live in
+device memory.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -81,7 +78,9 @@ class ReplicaTrainer:
         self.lr_dev = torch.full((1,), 0.01, device=dev)
         self.m, self.v, self.vhat = self.engine.adam_state()
         self.graphs = None
-        self.stream = torch.cuda.Stream(device=dev)
+        # PLD_STREAM_PRIO=1: the step's stream at high priority (side streams stay default)
+        prio = -1 if os.environ.get("PLD_STREAM_PRIO", "0") == "1" else 0
+        self.stream = torch.cuda.Stream(device=dev, priority=prio)
         self.side = torch.cuda.Stream(device=dev)  # per-bucket optimizer updates (N > 1)
 
     # ------------------------------------------------------------------ data
@@ -156,6 +155,14 @@ class ReplicaTrainer:
     # ------------------------------------------------------------------ data parallel
     BUCKET_BYTES = 8 << 20
 
+    def _dp_buckets(self):
+        """Reverse-order, tensor-aligned gradient buckets (dp.tensor_buckets), built once."""
+        if not hasattr(self, "_buckets"):
+            eng = self.engine
+            self._buckets = dp.tensor_buckets([off for _, _, off in eng.params.specs],
+                                              eng.grads.buf.numel(), self.BUCKET_BYTES)
+        return self._buckets
+
     def _dp_refresh_convs(self, lo, hi):
         """Trainable convs whose kernel lies in flat range [lo, hi)."""
         eng = self.engine
@@ -172,94 +179,55 @@ class ReplicaTrainer:
         for c in self._dp_refresh_convs(lo, hi):
             c.refresh()
 
-    def _dp_bucket(self, lo, hi):
-        """All-reduce grads[lo:hi) (async, ordered after the compute stream's work so far), then
-        on the side stream: wait for it and run the bucket's update."""
-        work = dp.allreduce_bucket(self.engine.grads.buf, lo, hi, self.pg)
-        with torch.cuda.stream(self.side):
-            work.wait()
-            self._dp_update(lo, hi)
-        self._dp_works.append(work)
-
-    def _dp_grad_ready(self, off):
-        """engine.backward hook: grads[off:] are final (dp.BucketSchedule decides)."""
-        b = self._dp_sched.ready(off)
-        if b is not None:
-            self._dp_bucket(*b)
-
-    def _step_dp(self):
-        """One data-parallel step (N > 1), eager, on self.stream (+ RCCL and the side stream)."""
-        eng = self.engine
-        self._sample()
-        eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
-        K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
-                          dpred=self.dpred, nll=self.nll, loss=self.loss, zero_dpred=True)
-        self.side.wait_stream(self.stream)
-        self._dp_sched = dp.BucketSchedule(eng.grads.buf.numel(), self.BUCKET_BYTES)
-        self._dp_works = []
-        eng.backward(self.dpred, grad_ready=self._dp_grad_ready)
-        self._dp_grad_ready(0)
-        # the step counter (Adam's bias correction, the next step's Philox keys) advances once
-        # every bucket's update has run; the next step's forward reads the updated filters
-        self.stream.wait_stream(self.side)
-        K.step_increment(self.step_dev)
-
-    def _capture_dp(self):
-        """Segmented capture of the N > 1 step (module docstring): the compute stream's launches
-        from the step start to the first bucket boundary, between boundaries, up to the last
-        one (offset 0: the end of the backward) are graphs `segs`; each bucket's Adam-AMSGrad +
-        filter refresh on the side stream is a graph in `bucket_graphs`."""
-        eng = self.engine
-        torch.cuda.synchronize()
-        segs, buckets = [], []
-        sched = dp.BucketSchedule(eng.grads.buf.numel(), self.BUCKET_BYTES)
-        cur = [None]
-
-        def boundary(off):
-            b = sched.ready(off)
-            if b is not None:
-                segs.append(cur[0].end())
-                buckets.append(b)
-                cur[0] = None if sched.done else K.Graph().begin()
-
-        with torch.cuda.stream(self.stream):
-            cur[0] = K.Graph().begin()
-            try:
-                self._sample()
-                eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
-                K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
-                                  dpred=self.dpred, nll=self.nll, loss=self.loss,
-                                  zero_dpred=True)
-                eng.backward(self.dpred, grad_ready=boundary)
-                boundary(0)
-            except BaseException:
-                if cur[0] is not None:
-                    cur[0].end(failed=True)
-                raise
-        assert sched.done and len(segs) == len(buckets), "backward never reached offset 0"
-        with torch.cuda.stream(self.side):
-            graphs = [K.Graph().capture(lambda lo=lo, hi=hi: self._dp_update(lo, hi))
-                      for lo, hi in buckets]
-        torch.cuda.synchronize()
-        self.graphs = segs
-        self.bucket_graphs = list(zip(buckets, graphs))
-
-    def _replay_dp(self):
-        """One captured N > 1 step on self.stream (the caller's current stream)."""
-        eng = self.engine
+    def _dp_exchange(self, updates=None):
+        """After the backward (on self.stream): each bucket's all-reduce (RCCL, ordered after
+        the backward by c10d) and, on the side stream as soon as it lands, that bucket's update
+        — eager (_dp_update) or its captured graph (updates[i]); the updates of the first
+        buckets overlap the all-reduces of the later ones. Then the step counter advances (Adam's
+        bias correction and the next step's Philox keys read it)."""
+        grads = self.engine.grads.buf
         self.side.wait_stream(self.stream)
         works = []
-        for seg, ((lo, hi), upd) in zip(self.graphs, self.bucket_graphs):
-            seg.launch()
-            # c10d orders the collective after the current stream (self.stream) = this segment
-            work = dp.allreduce_bucket(eng.grads.buf, lo, hi, self.pg)
+        for i, (lo, hi) in enumerate(self._dp_buckets()):
+            work = dp.allreduce_bucket(grads, lo, hi, self.pg)
             with torch.cuda.stream(self.side):
                 work.wait()
-                upd.launch()
+                if updates is None:
+                    self._dp_update(lo, hi)
+                else:
+                    updates[i].launch()
             works.append(work)
         self._dp_works = works
         self.stream.wait_stream(self.side)
         K.step_increment(self.step_dev)
+
+    def _step_dp(self):
+        """One data-parallel step (N > 1), eager, on self.stream (+ RCCL and the side stream)."""
+        self._sample()
+        self._fwd_bwd()
+        self._dp_exchange()
+
+    def _capture_dp(self):
+        """N > 1 capture: the compute (sampler, forward, ListMLE, backward with its weight-
+        gradient side stream) is one graph; each bucket's update another, on the side stream.
+        A replay launches the compute graph, then issues the bucket all-reduces through
+        torch.distributed between the update graphs (the collectives stay outside the graphs:
+        RCCL's own stream, c10d's stream dependencies and work objects run as they do eagerly).
+        Per step the host issues 1 + 2 x buckets launches and the collectives."""
+        torch.cuda.synchronize()
+        with torch.cuda.stream(self.stream):
+            step = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd()))
+        with torch.cuda.stream(self.side):
+            upd = [K.Graph().capture(lambda lo=lo, hi=hi: self._dp_update(lo, hi))
+                   for lo, hi in self._dp_buckets()]
+        torch.cuda.synchronize()
+        self.graphs = [step]
+        self.bucket_graphs = upd
+
+    def _replay_dp(self):
+        """One captured N > 1 step on self.stream (the caller's current stream)."""
+        self.graphs[0].launch()
+        self._dp_exchange(self.bucket_graphs)
 
     # ------------------------------------------------------------------ driving
     def step_eager(self, lr):

@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pldepth_amd.dp import BucketSchedule, allreduce_bucket, shard
+from pldepth_amd.dp import allreduce_bucket, shard, tensor_buckets
 
 
 def _free_port():
@@ -45,14 +45,10 @@ def _spawn(fn, world=2):
 
 
 def _exchange(flat, offsets, bucket_bytes, group=None):
-    """The trainer's exchange over one simulated backward: the backward reports decreasing
-    'grads[off:] final' offsets; every bucket the schedule releases is all-reduced async."""
-    sched, works, buckets = BucketSchedule(flat.numel(), bucket_bytes), [], []
-    for off in list(offsets) + [0]:
-        b = sched.ready(off)
-        if b is not None:
-            buckets.append(b)
-            works.append(allreduce_bucket(flat, *b, group))
+    """The trainer's exchange (trainer._dp_exchange): every tensor-aligned bucket all-reduced
+    async in reverse order, then waited on."""
+    buckets = tensor_buckets(offsets, flat.numel(), bucket_bytes)
+    works = [allreduce_bucket(flat, lo, hi, group) for lo, hi in buckets]
     for w in works:
         w.wait()
     return buckets
@@ -69,22 +65,24 @@ def test_bucketed_allreduce_sums_every_element():
     ref = np.arange(1003, dtype=np.float32) * 3
     for r in (0, 1):
         np.testing.assert_array_equal(out[r][0], ref)
-    # >= 64 floats pending releases a bucket; offset 0 always closes the last one
+    # >= 64 floats per bucket, boundaries at tensor starts; offset 0 closes the last one
     assert out[0][1] == [(900, 1003), (700, 900), (300, 700), (100, 300), (5, 100), (0, 5)]
     assert out[0][1] == out[1][1]
 
 
-def test_bucket_schedule_tiles_the_buffer():
+def test_tensor_buckets_tile_the_buffer():
     rng = np.random.default_rng(3)
     for _ in range(50):
         n = int(rng.integers(1, 10000))
-        offs = sorted(set(rng.integers(0, n, int(rng.integers(0, 40))).tolist()), reverse=True)
-        s = BucketSchedule(n, bucket_bytes=int(rng.integers(4, 4000)))
-        got = [b for b in (s.ready(o) for o in offs + [0]) if b is not None]
-        assert s.done and got[0][1] == n and got[-1][0] == 0
+        offs = sorted(set(rng.integers(0, n, int(rng.integers(0, 40))).tolist()))
+        got = tensor_buckets(offs, n, bucket_bytes=int(rng.integers(4, 4000)))
+        assert got[0][1] == n and got[-1][0] == 0
         assert all(a[0] == b[1] for a, b in zip(got, got[1:]))  # contiguous, reverse order
         assert all(lo < hi for lo, hi in got)
-        assert s.ready(0) is None  # nothing left after the last bucket
+        starts = set(offs) | {0}
+        assert all(lo in starts for lo, _ in got)  # no tensor spans two buckets
+    with pytest.raises(ValueError):
+        tensor_buckets([10], 10)
 
 
 def test_shard_layout():

@@ -1,9 +1,9 @@
 """The data-parallel ReplicaTrainer path (N > 1) on the one leased GPU: two processes, the gloo
 backend on device tensors (RCCL needs one GPU per rank; the driver's 8-GPU runs use it).
 
-Each rank owns half of a global batch of 4 and steps with the overlapped per-bucket all-reduce +
-Adam: step 1 eager (trainer._step_dp), step 2 replayed from the segmented capture
-(trainer._capture_dp / _replay_dp). After 2 steps its parameters must equal a single-process run that
+Each rank owns half of a global batch of 4 and steps with the per-bucket all-reduce + Adam:
+step 1 eager (trainer._step_dp), step 2 replayed from the capture (trainer._capture_dp /
+_replay_dp). After 2 steps its parameters must equal a single-process run that
 computes both shards' gradients, sums them and applies Adam with grad_scale 1/2 — the mean of the
 replica gradients, per-replica BN statistics (MirroredStrategy semantics)."""
 import os
@@ -54,8 +54,8 @@ def _rank_main(rank, port, q, model):
         tr.synchronize()
         g1 = tr.engine.grads.buf.cpu().numpy()  # the all-reduced (summed) step-1 gradient
         p1 = tr.engine.params.buf.cpu().numpy()
-        tr.capture()  # segment graphs + per-bucket update graphs, collectives between them
-        assert tr.graphs is not None and len(tr.graphs) == len(tr.bucket_graphs) >= 2
+        tr.capture()  # compute graph + per-bucket update graphs, collectives between them
+        assert tr.graphs is not None and len(tr.bucket_graphs) >= 2
         for _ in range(STEPS - 1):
             tr.step(0.01)
         tr.synchronize()

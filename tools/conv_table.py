@@ -43,10 +43,13 @@ def timed_step(tr, lr):
 
     for n in orig:
         setattr(K, n, wrap(n))
+    overlap = getattr(tr.engine, "overlap_wgrad", False)
+    tr.engine.overlap_wgrad = False  # one stream: the events bracket each conv alone
     try:
         tr.step_eager(lr)
         st.synchronize()
     finally:
+        tr.engine.overlap_wgrad = overlap
         for n, f in orig.items():
             setattr(K, n, f)
     return [(m, M, N, Kd, k, t, e0.elapsed_time(e1)) for m, M, N, Kd, k, t, e0, e1 in recs]

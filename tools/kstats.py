@@ -1,6 +1,6 @@
 """Per-kernel statistics from a rocprofv3 kernel-trace SQLite database (rocpd schema).
 
-    python tools/kstats.py gpurun_out/prof/run_results.db [--csv out.csv] [--top N]
+    python tools/kstats.py gpurun_out/prof/run_results.db|<csv dir> [--csv out.csv] [--top N]
         [--marker adam_amsgrad_dev_kernel --steps 8 --skip 1]
 
 With --marker, only dispatches inside the last `steps` marker-to-marker windows (dropping the
@@ -14,6 +14,17 @@ import sys
 
 
 def load(db):
+    """(name, start, end) per dispatch from a rocpd SQLite database, a rocprofv3 csv output
+    directory (its *kernel_trace.csv) or that csv file."""
+    import glob
+    import os
+    if os.path.isdir(db):
+        db = sorted(glob.glob(os.path.join(db, "*kernel_trace.csv")))[0]
+    if db.endswith(".csv"):
+        with open(db) as f:
+            rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                    for r in csv.DictReader(f)]
+        return sorted(rows, key=lambda r: r[1])
     c = sqlite3.connect(db)
     return c.execute("select name, start, end from kernels order by start").fetchall()
 
