@@ -1267,7 +1267,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
   if (mode == 2)
     return wgrad_patch_geom(a) ? (pld__x3_patch_wgrad_cw(a->cout) == 64
                                       ? "conv_x3_patch_wgrad64_kernel"
-                                      : "conv_x3_patch_wgrad_kernel")
+                                      : "conv_x3_patch_wgrad_pc_kernel")
                                : "conv_x3_kernel";
   // FWD view (dgrad: the input is dY, cout channels, one source)
   const int c1 = mode == 0 ? a->c1 : a->cout, c2 = mode == 0 ? a->c2 : 0;

@@ -968,6 +968,193 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad_kernel(GemmConvParams
     }
 }
 
+// The same contraction, warp-specialised (round 3). The uniform kernel above holds 9 accumulator
+// tiles (144 VGPRs) + the next tile's loads in every wave at 2 waves per SIMD, which leaves one
+// fragment register set: every MFMA pair waits on its own transposed LDS read (lgkmcnt(0)),
+// and all waves split + store the next tile together while the matrix pipes idle (MFMA 31 %
+// busy). Here waves 0-3 only compute — wave c owns output rows 2c, 2c+1 of the 8 x 32 tile (four
+// 16-pixel k-steps, all 9 taps), with the next tap's A fragments and the next k-step's dY
+// fragments read while the current ones multiply — and waves 4-7 only stage: global loads two
+// tiles ahead in registers, bf16 hi/lo split, LDS stores into the other buffer. One barrier per
+// tile; the 4 consumers' partial sums meet in LDS in a fixed order (deterministic).
+__device__ __forceinline__ void pw_frag_pair(const unsigned char* plane, int plane_bytes, int row0,
+                                             int lane, bf16x8& hi, bf16x8& lo) {
+  hi = tr_frag_rows(plane, row0, lane);
+  lo = tr_frag_rows(plane + plane_bytes, row0, lane);
+}
+
+__global__ __launch_bounds__(512) void conv_x3_patch_wgrad_pc_kernel(GemmConvParams p, int tiles,
+                                                                     int tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PW_STAGE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  const bool s2 = q >= p.kc1;
+  const int cb = (s2 ? q - p.kc1 : q) * 32;
+  const int cs = s2 ? p.c2 : p.c1;
+  const int nv = min(32, cs - cb);
+  const int n0 = nb * 32;
+  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
+  const int n = t_end - t_begin;
+
+  floatx16 acc[9];  // consumers only (the producers' path never defines it: no registers)
+  if (wave >= 4) {  // ------------------------------------------------------------ producer
+    const int ptid = threadIdx.x - 256;
+    const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
+    const long img_in = (long)p.h * p.w * cs;
+    const long img_out = (long)p.oh * p.ow;
+    const float* xsrc = s2 ? p.x2 : p.x1;
+    constexpr int EA = P_PIX * 8, IA = (EA + 255) / 256;  // patch: 4-channel quads
+    constexpr int EB = PT_H * PT_W * 8, IB = EB / 256;    // dY: 4-channel quads
+    struct Stage {
+      float4 a[IA], b[IB];
+    };
+    auto load = [&](int t, Stage& st) {
+      t = min(t, t_end - 1);  // past the end: a harmless re-load of the last tile
+      const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
+      const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int e = ptid + 256 * i;
+        const int px = e >> 3, c4 = (e & 7) * 4;
+        const int py = px / P_W, pxx = px - py * P_W;
+        const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+        const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
+                        (unsigned)ix < (unsigned)p.w;
+        st.a[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
+      }
+      const __amdgpu_buffer_rsrc_t rd =
+          make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int e = ptid + 256 * i;
+        const int k = e >> 3, c4 = (e & 7) * 4;
+        const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
+        const bool ok = oy < p.oh && ox < p.ow && n0 + c4 < p.N;
+        st.b[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
+      }
+    };
+    auto store = [&](int buf, const Stage& st) {
+      unsigned char* A = smem + buf * PW_STAGE;
+      unsigned char* B = A + 2 * PW_A;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int e = ptid + 256 * i;
+        if (e < EA) {
+          unsigned h0, l0, h1, l1;
+          split2(st.a[i].x, st.a[i].y, h0, l0);
+          split2(st.a[i].z, st.a[i].w, h1, l1);
+          const int o = (e >> 3) * 64 + (e & 7) * 8;
+          *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
+          *reinterpret_cast<u32x2*>(A + PW_A + o) = u32x2{l0, l1};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int e = ptid + 256 * i;
+        unsigned h0, l0, h1, l1;
+        split2(st.b[i].x, st.b[i].y, h0, l0);
+        split2(st.b[i].z, st.b[i].w, h1, l1);
+        const int o = (e >> 3) * 64 + (e & 7) * 8;
+        *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(B + PW_B + o) = u32x2{l0, l1};
+      }
+    };
+    if (n > 0) {
+      // one register stage (a tile's loads land during the previous tile's ~3.5k MFMA
+      // cycles); barriers 1 + n, matching the consumers
+      Stage st;
+      load(t_begin, st);
+      store(0, st);
+      load(t_begin + 1, st);
+      lds_barrier();
+      for (int i = 0;; ++i) {
+        store((i + 1) & 1, st);  // tile i+1 while the consumers multiply tile i
+        load(t_begin + i + 2, st);
+        lds_barrier();
+        if (i + 1 >= n) break;
+      }
+    }
+  } else {  // ----------------------------------------------------------------- consumer
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    if (n > 0) {
+      lds_barrier();
+      for (int t = 0; t < n; ++t) {
+        const unsigned char* A = smem + (t & 1) * PW_STAGE;
+        const unsigned char* B = A + 2 * PW_A;
+        // k-step s: output row 2 wave + (s >> 1), pixels 16 (s & 1) .. +15
+        bf16x8 bh, bl, ah, al, nh, nl;
+        pw_frag_pair(B, PW_B, 32 * (2 * wave), lane, bh, bl);
+        pw_frag_pair(A, PW_A, (2 * wave) * P_W, lane, ah, al);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 2 * wave + (s >> 1), px0 = 16 * (s & 1);
+          bf16x8 bh2 = bh, bl2 = bl;
+          if (s < 3) {
+            const int s1 = s + 1;
+            pw_frag_pair(B, PW_B, 32 * (2 * wave + (s1 >> 1)) + 16 * (s1 & 1), lane, bh2, bl2);
+          }
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) {
+            // the next A fragments (next tap, or tap 0 of the next k-step) in flight during
+            // this tap's three products
+            if (tap < 8) {
+              const int t1 = tap + 1;
+              pw_frag_pair(A, PW_A, (row + t1 / 3) * P_W + px0 + t1 % 3, lane, nh, nl);
+            } else if (s < 3) {
+              const int s1 = s + 1;
+              pw_frag_pair(A, PW_A, (2 * wave + (s1 >> 1)) * P_W + 16 * (s1 & 1), lane, nh, nl);
+            }
+            // the reads above issue before this tap's products (then the 3 MFMAs); one
+            // fragment set ahead and no more: the scheduler otherwise hoists every read of the
+            // tile (register blow-up, spills)
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
+            ah = nh;
+            al = nl;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          bh = bh2;
+          bl = bl2;
+        }
+        lds_barrier();
+      }
+    }
+  }
+  // the 4 consumers' partial sums through LDS: each writes its 9 tiles to its own slot, then
+  // all 512 threads add the 4 slots per element in a fixed order ((0 + 1) + (2 + 3)) and store
+  // (deterministic; no wave holds two sets of accumulators)
+  constexpr int SLOT = 9 * 16 * 64;  // floats: tile t, register r, lane
+  static_assert(4 * SLOT * 4 <= 2 * PW_STAGE, "reduction slots fit the staging LDS");
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();  // the last tile's LDS reads are done
+  if (wave < 4) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[wave * SLOT + (t * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
+  for (int e = threadIdx.x; e < SLOT; e += 512) {
+    const int ln = e & 63, r = (e >> 6) & 15, t = e >> 10;
+    const int h = ln >> 5, col = n0 + (ln & 31);
+    const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (col >= p.N || ci >= nv) continue;
+    const float v = (red[e] + red[SLOT + e]) + (red[2 * SLOT + e] + red[3 * SLOT + e]);
+    const long m = (long)t * p.C + (s2 ? p.c1 : 0) + cb + ci;
+    float* dst = out + m * p.N + col;
+    *dst = (p.zstride == 0 && p.acc1) ? *dst + v : v;
+  }
+}
+
 // The same for 64 output channels per workgroup (N > 32: the 240- and 144-wide decoder convs):
 // the input patch of a tile is staged ONCE for both 32-wide cout tiles (the 32-wide kernel
 // re-stages it per cout tile: 8 / 5 times for N = 240 / 144 — fetch-bound, PMC: 2.9x the
@@ -1291,8 +1478,13 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
     return check_launch("conv_x3_patch_wgrad64_kernel");
   }
   dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
+#ifdef X3_PW_UNIFORM  // the round-2 uniform-role kernel (A/B builds only)
   x3::conv_x3_patch_wgrad_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
   return check_launch("conv_x3_patch_wgrad_kernel");
+#else
+  x3::conv_x3_patch_wgrad_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
+  return check_launch("conv_x3_patch_wgrad_pc_kernel");
+#endif
 }
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {

@@ -128,8 +128,8 @@ class EffNetFF:
         # at the end of the backward: 1 = each forked once its layer's pre-BN gradient exists
         # (concurrent with the rest of the decoder chain), 2 = all forked after the last decoder
         # dgrad (concurrent with the encoder backward, which has no weight gradients of its
-        # own); 0 = in line
-        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "0"))
+        # own; +0.7 % img/s, while mode 1 costs 1.5 %: profiles/r03_overlap_ab.txt); 0 = in line
+        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
 
     # ------------------------------------------------------------------ graph structure
     def _build_spec(self):

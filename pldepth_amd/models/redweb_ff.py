@@ -80,7 +80,7 @@ class RedWebFF:
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
-        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "0"))
+        self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
         self._side = False
         self.seed = seed
 
@@ -374,14 +374,18 @@ class RedWebFF:
                            math=self._math(conv, oh, ow))
         if conv.trainable:
             if self._side:
-                wstream, fork = self._wgrad_side()
-                fork[conv.name].record(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(wstream):
-                    wstream.wait_event(fork[conv.name])
+                def wg(args=args, gy=gy, rows=self.B * oh * ow, conv=conv):
                     K.conv2d_wgrad(args, gy, conv.dw)
                     if conv.db is not None:
-                        K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db,
-                                      ws_key="reduce_side")
+                        K.channel_sum(gy, rows, conv.cout, conv.db, ws_key="reduce_side")
+                if self.overlap_wgrad == 2:
+                    self._deferred.append(wg)
+                else:
+                    wstream, fork = self._wgrad_side()
+                    fork[conv.name].record(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(wstream):
+                        wstream.wait_event(fork[conv.name])
+                        wg()
             else:
                 K.conv2d_wgrad(args, gy, conv.dw)
                 if conv.db is not None:
@@ -401,6 +405,7 @@ class RedWebFF:
         # decoder weight gradients on a side stream (EffNetFF.backward); a data-parallel caller
         # (grad_ready) keeps the single-stream order
         self._side = bool(self.overlap_wgrad) and grad_ready is None
+        self._deferred = []
         main = torch.cuda.current_stream(self.device)
         H, W = self.H, self.W
         h, w = H // 2, W // 2
@@ -417,6 +422,15 @@ class RedWebFF:
             up = A["conv5_up"] if i == 0 else A[self.ffls[i - 1]["name"] + "/out"]
             gup = G["conv5_up"] if i == 0 else G[self.ffls[i - 1]["name"] + "/out"]
             self._ffl_bwd(d, A[d["tap"]], G[d["tap"]], up, gup)
+        if self._side and self._deferred:  # overlap mode 2: beside the encoder backward
+            wstream, fork = self._wgrad_side()
+            ev = fork[self.aol0.name]
+            ev.record(main)
+            with torch.cuda.stream(wstream):
+                wstream.wait_event(ev)
+                for wg in self._deferred:
+                    wg()
+        self._deferred = []
         ready(min(off for n, _, off in self.params.specs
                   if any(c.trainable and n == c.wk for c in self.convs)))
         K.upsample2x_bwd(G["conv5_up"], G["conv5_block3_out"])

@@ -12,13 +12,16 @@
 * cfg5: the full-size ListMLE (B=32, R=1000, L=64: 2,048,000 list elements, heavy duplicate
   pixels) against oracle/listmle.py.
 
-Gradient bar (BASELINE.json: 1e-3 relative): wherever the fp32 restatement of the reference
-semantics itself lands within 1e-3 of fp64, the HIP gradient must too. Where it does not — and
-at test batch sizes that is almost every tensor: training-mode BN over a batch of 2 cancels most
-of each incoming gradient, so the fp32 restatement itself lands ~1 % (global rel-L2) from fp64 —
-the HIP gradient must be no further from fp64 than 4x the fp32 restatement per tensor (bf16x3
-products carry ~2^8 the rounding of fp32 ones; measured worst ratio 3.5x) and 2x over all
-tensors together. Reports of every tensor are written to $PLD_REPORT_DIR when set.
+Gradient bar (BASELINE.json: 1e-3 relative): per tensor max(1e-3, 4x the fp32 restatement's own
+error) — wherever the fp32 restatement of the reference semantics lands within 2.5e-4 of fp64,
+the HIP gradient must be within 1e-3 — and over all tensors together a global rel-L2 within
+max(1e-3, 2x the fp32 restatement's). The gradients of the reference semantics are themselves
+ill-conditioned at the 1e-3 level: training-mode BN cancels most of each incoming gradient, and
+an exact fp32 implementation lands ~1 % (median per tensor) from fp64 at batch 2 AND at the
+bench's batch 32 (ff_effnet 5 of 98 tensors within 1e-3, ff_redweb 3 of 237; profiles/r03_parity).
+bf16x3 products carry ~2^8 the rounding of fp32 ones; measured HIP / fp32-restatement error
+ratios: median 0.90 (ff_effnet) / 1.03 (ff_redweb) at batch 32, worst 2.3. Reports of every tensor
+are written to $PLD_REPORT_DIR when set.
 """
 import json
 import os
@@ -81,7 +84,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero):
     rows, fails = {}, []
     for k in keys:
         e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64[k])
-        bar = TOL if e32 <= TOL else 4.0 * e32
+        bar = max(TOL, 4.0 * e32)
         rows[k] = {"hip": e_hip, "fp32_restatement": e32, "bar": bar}
         if e_hip > bar:
             fails.append((k, e_hip, e32))
@@ -445,6 +448,7 @@ def test_batch32_bench_policy(cuda, model):
     print(errs, bars)
     assert all(errs[n] < bars[n] for n in errs), (errs, bars)
     glob = check_gradients(f"{model}_b32_auto_grads", hip_grads, g64, g32, zero)
-    # at the bench's batch the BN reductions span 16x the values of the batch-2 tests: the
-    # 1e-3 branch of the bar governs most tensors
-    assert glob["tensors_fp32_within_1e-3"] >= glob["tensors"] // 2, glob
+    # HIP is as close to fp64 as an exact fp32 implementation of the reference semantics: no
+    # more tensors outside 1e-3 than the fp32 restatement has, give or take 10 % of them
+    assert glob["tensors_hip_within_1e-3"] >= glob["tensors_fp32_within_1e-3"] - \
+        max(1, glob["tensors"] // 10), glob
