@@ -1275,8 +1275,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
                    a->in_scale == nullptr && a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 &&
                    a->pad_l <= 2;
   if (!geo) return "conv_x3_kernel";
-  if (c1 == 32 && c2 == 0)  // schedules 0, 1 (32 / 64 columns): the persistent kernel
-    return cfg <= 1 ? "conv_x3_patch_pc_kernel" : "conv_x3_patch_kernel";
+  if (c1 == 32 && c2 == 0) return "conv_x3_patch_kernel";
   return (cfg == 0 && c1 % 16 == 0 && c2 % 16 == 0) ? "conv_x3_patch_mc_pc_kernel"
                                                       : "conv_x3_kernel";
 }

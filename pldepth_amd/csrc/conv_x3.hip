@@ -660,177 +660,6 @@ __global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
   }
 }
 
-// The 32-channel-input patch conv, persistent and warp-specialised (round 3): the filter of
-// the workgroup's BN output channels is staged ONCE (the one-tile kernel above re-stages it for
-// every 8 x 32 tile: ~half of its staging bytes), then the workgroup walks a contiguous run of
-// tiles (horizontal neighbours share halo columns in L2) with the patch double-buffered: waves
-// 4-7 load tile i+2 into registers and split + store tile i+1 while waves 0-3 multiply tile i
-// (two output rows each, the next fragments read during the current products) and store it.
-template <int BN>
-__global__ __launch_bounds__(512) void conv_x3_patch_pc_kernel(GemmConvParams p, int tiles,
-                                                                int tiles_per_wg) {
-  using S = PatchSmem<BN>;
-  constexpr int TN = BN / 32;
-  constexpr int PSTAGE = 2 * S::A_PLANE;  // one patch buffer (hi + lo planes)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PSTAGE + 2 * S::B_PLANE];
-  unsigned char* Bh = smem + 2 * PSTAGE;
-  unsigned char* Bl = Bh + S::B_PLANE;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
-  const int n0 = blockIdx.y * BN;
-  const int t_begin = blockIdx.x * tiles_per_wg, t_end = min(tiles, t_begin + tiles_per_wg);
-  const int n = t_end - t_begin;
-  if (n <= 0) return;  // uniform over the workgroup
-  auto tile_geo = [&](int t, int& img, int& oy0, int& ox0) {
-    const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y;
-    img = r1 / tiles_y;
-    oy0 = ty0 * PT_H;
-    ox0 = tx0 * PT_W;
-  };
-
-  floatx16 acc[2][TN];  // compute waves only
-  if (wave >= 4) {  // ------------------------------------------------------------ staging
-    const int ptid = threadIdx.x - 256;
-    {  // the filter, once
-      const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.bsplit, (long)p.N * p.K * 4);
-      constexpr int EB = 9 * BN * 8;
-      for (int e = ptid; e < EB; e += 256) {
-        const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
-        const int tap = nt / BN, nn = nt - tap * BN;
-        const bool ok = n0 + nn < p.N;
-        const float4 v = bload4(
-            rb, ok ? (unsigned)(((n0 + nn) * p.K + tap * 32 + 8 * c) * 4 + 16 * half) : OOB);
-        *reinterpret_cast<float4*>((half ? Bl : Bh) + tap * S::B_TAP + chunk_off(nn, c)) = v;
-      }
-    }
-    const long img_elems = (long)p.h * p.w * 32;
-    constexpr int EA = P_PIX * 8, IA = (EA + 255) / 256;
-    float4 va[IA];
-    auto load = [&](int t) {
-      t = min(t, t_end - 1);  // past the end: a harmless re-load of the last tile
-      int img, oy0, ox0;
-      tile_geo(t, img, oy0, ox0);
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.x1 + img * img_elems, img_elems * 4);
-#pragma unroll
-      for (int i = 0; i < IA; ++i) {
-        const int e = ptid + 256 * i;
-        const int px = e >> 3, q = e & 7;
-        const int py = px / P_W, pxx = px - py * P_W;
-        const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
-        const bool ok = e < EA && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-        va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * 32 + 4 * q) * 4) : OOB);
-      }
-    };
-    auto store = [&](int buf) {
-      unsigned char* Ah = smem + buf * PSTAGE;
-      unsigned char* Al = Ah + S::A_PLANE;
-#pragma unroll
-      for (int i = 0; i < IA; ++i) {
-        const int e = ptid + 256 * i;
-        if (e < EA) {
-          const int px = e >> 3, q = e & 7;
-          unsigned h0, l0, h1, l1;
-          split2(va[i].x, va[i].y, h0, l0);
-          split2(va[i].z, va[i].w, h1, l1);
-          const int o = chunk_off(px, q >> 1) + 8 * (q & 1);
-          *reinterpret_cast<u32x2*>(Ah + o) = u32x2{h0, h1};
-          *reinterpret_cast<u32x2*>(Al + o) = u32x2{l0, l1};
-        }
-      }
-    };
-    // barriers: 1 + n, matching the compute waves
-    load(t_begin);
-    store(0);
-    load(t_begin + 1);
-    lds_barrier();
-    for (int i = 0;; ++i) {
-      store((i + 1) & 1);
-      load(t_begin + i + 2);
-      lds_barrier();
-      if (i + 1 >= n) break;
-    }
-    return;
-  }
-  // ------------------------------------------------------------------------ compute
-  const int h = lane >> 5, l32 = lane & 31;
-  lds_barrier();
-  for (int i = 0; i < n; ++i) {
-    const unsigned char* Ah = smem + (i & 1) * PSTAGE;
-    const unsigned char* Al = Ah + S::A_PLANE;
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[rr][b][r] = 0.f;
-    auto frags = [&](int j, bf16x8 (&a)[4], bf16x8 (&bf)[2 * TN]) {
-      const int tap = j >> 1, s = j & 1;
-      const int r0 = (2 * wave + tap / 3) * P_W + l32 + tap % 3;
-      a[0] = lds_frag(Ah, r0, 2 * s + h);
-      a[1] = lds_frag(Al, r0, 2 * s + h);
-      a[2] = lds_frag(Ah, r0 + P_W, 2 * s + h);
-      a[3] = lds_frag(Al, r0 + P_W, 2 * s + h);
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        bf[2 * b] = lds_frag(Bh + tap * S::B_TAP, b * 32 + l32, 2 * s + h);
-        bf[2 * b + 1] = lds_frag(Bl + tap * S::B_TAP, b * 32 + l32, 2 * s + h);
-      }
-    };
-    bf16x8 a[4], bf[2 * TN], na[4], nbf[2 * TN];
-    frags(0, a, bf);
-#pragma unroll
-    for (int j = 0; j < 18; ++j) {
-      if (j < 17) frags(j + 1, na, nbf);
-      __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * TN, 0);  // next step's reads
-      __builtin_amdgcn_sched_group_barrier(0x008, 6 * TN, 0);      // this step's products
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          floatx16& c = acc[rr][b];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 * rr + 1], bf[2 * b], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 * rr], bf[2 * b + 1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 * rr], bf[2 * b], c, 0, 0, 0);
-        }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = na[u];
-#pragma unroll
-      for (int u = 0; u < 2 * TN; ++u) bf[u] = nbf[u];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // epilogue of tile i (global stores only: the next tile's LDS is already staged)
-    int img, oy0, ox0;
-    tile_geo(t_begin + i, img, oy0, ox0);
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int oy = oy0 + 2 * wave + rr;
-      if (oy >= p.oh) continue;
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = n0 + b * 32 + l32;
-        if (col >= p.N) continue;
-        const float bias = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ox = ox0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (ox >= p.ow) continue;
-          const long row = ((long)img * p.oh + oy) * p.ow + ox;
-          const float v = acc[rr][b][r] + bias;
-          if (col < p.split) {
-            float* dst = p.out1 + row * p.ld1 + col;
-            *dst = p.acc1 ? *dst + v : v;
-          } else {
-            float* dst = p.out2 + row * p.ld2 + (col - p.split);
-            *dst = p.acc2 ? *dst + v : v;
-          }
-        }
-      }
-    }
-    lds_barrier();
-  }
-}
-
 // The same for inputs of several 32-channel chunks (C % 16 == 0 per source; a concat's sources
 // chunked separately, a ragged 16-channel chunk masked): 32 output channels per workgroup, the
 // (patch, filter) stage of chunk i+1 loaded into registers while chunk i is multiplied, double
@@ -1789,19 +1618,6 @@ extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream) {
 #endif
   }
   const int bn = x3::kPatchBN[cfg];
-#ifndef X3_PATCH_UNIFORM
-  if (bn <= 64) {  // persistent: one workgroup per CU (LDS 124 / 161 KB), filter staged once
-    const int ntile_n = (int)cdiv(p->N, bn);
-    const int wgs = std::max(1, std::min(tiles, 256 / ntile_n));
-    const int tpw = (int)cdiv(tiles, wgs);
-    dim3 g((unsigned)cdiv(tiles, tpw), ntile_n);
-    if (bn == 32)
-      x3::conv_x3_patch_pc_kernel<32><<<g, 512, 0, as_stream(stream)>>>(*p, tiles, tpw);
-    else
-      x3::conv_x3_patch_pc_kernel<64><<<g, 512, 0, as_stream(stream)>>>(*p, tiles, tpw);
-    return check_launch("conv_x3_patch_pc_kernel");
-  }
-#endif
   dim3 grid(tiles, cdiv(p->N, bn));
   hipStream_t st = as_stream(stream);
   switch (cfg) {
