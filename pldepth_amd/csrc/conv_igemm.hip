@@ -822,6 +822,7 @@ extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
 extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream);
 extern "C" int pld__x3_patch_wgrad_cw(int N);
+extern "C" int pld__x3_patch_wgrad_th(int N);
 constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
@@ -1266,7 +1267,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
   const int cfg = a->tile - 2 * pld__x3_num_cfg();
   if (mode == 2)
     return wgrad_patch_geom(a) ? (pld__x3_patch_wgrad_cw(a->cout) == 64
-                                      ? "conv_x3_patch_wgrad64_kernel"
+                                      ? "conv_x3_patch_wgrad64_pc_kernel"
                                       : "conv_x3_patch_wgrad_pc_kernel")
                                : "conv_x3_kernel";
   // FWD view (dgrad: the input is dY, cout channels, one source)
@@ -1447,7 +1448,7 @@ static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& spl
   }
   if (patch_out) *patch_out = patch;
   if (patch) {  // patch schedule: workgroups = chunks x cout tiles x splits, ~512 in all
-    const long tiles = (long)cdiv(a->ow, 32) * cdiv(a->oh, 8) * a->n;
+    const long tiles = (long)cdiv(a->ow, 32) * cdiv(a->oh, pld__x3_patch_wgrad_th(N)) * a->n;
     const long blocks = (long)(cdiv(a->c1, 32) + cdiv(a->c2, 32)) *
                         cdiv(N, pld__x3_patch_wgrad_cw(N));
     long s = std::max<long>(1, (512 + blocks - 1) / blocks);

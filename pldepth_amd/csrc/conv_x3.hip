@@ -1502,6 +1502,196 @@ __global__ __launch_bounds__(PW64_T) void conv_x3_patch_wgrad64_kernel(GemmConvP
     }
 }
 
+// The 64-cout weight gradient in the producer/consumer form of conv_x3_patch_wgrad_pc_kernel.
+// Double-buffering needs a smaller tile than the 8 x 32 one above (two 107 KB stages do not fit):
+// 4 x 32 output pixels, a 6 x 34 input patch (26 KB) + the [128 px][64 co] dY image (32 KB) per
+// stage. Waves 0-3 compute: wave c = (cout tile c & 1, output rows 2 (c >> 1), +1), all 9 taps
+// (9 accumulators, the next fragments read under the current products); waves 4-7 stage the next
+// tile. The two row pairs of a cout tile meet in LDS in a fixed order (deterministic). The
+// 4-row tile also fits the 28-row decoder maps exactly (8 rows: 4 tiles, 12.5 % padding).
+constexpr int Q_H = 4, Q_PH = Q_H + 2, Q_PIX = Q_PH * P_W;
+constexpr int Q_A = Q_PIX * 64;        // patch plane: [204 px][32 ch] bf16
+constexpr int Q_B = Q_H * PT_W * 128;  // dY plane: [128 px][64 co] bf16
+constexpr int Q_STAGE = 2 * Q_A + 2 * Q_B;
+
+__global__ __launch_bounds__(512) void conv_x3_patch_wgrad64_pc_kernel(GemmConvParams p,
+                                                                       int tiles,
+                                                                       int tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Q_STAGE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  const bool s2 = q >= p.kc1;
+  const int cb = (s2 ? q - p.kc1 : q) * 32;
+  const int cs = s2 ? p.c2 : p.c1;
+  const int nv = min(32, cs - cb);
+  const int n0 = nb * 64;
+  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
+  const int n = t_end - t_begin;
+  const int ct = wave & 1, rp = (wave >> 1) & 1;
+
+  floatx16 acc[9];
+  if (wave >= 4) {  // ------------------------------------------------------------ producer
+    const int ptid = threadIdx.x - 256;
+    const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + Q_H - 1) / Q_H;
+    const long img_in = (long)p.h * p.w * cs;
+    const long img_out = (long)p.oh * p.ow;
+    const float* xsrc = s2 ? p.x2 : p.x1;
+    constexpr int EA = Q_PIX * 8, IA = (EA + 255) / 256;  // patch: 4-channel quads
+    constexpr int EB = Q_H * PT_W * 16, IB = EB / 256;    // dY: 4-cout quads
+    struct Stage {
+      float4 a[IA], b[IB];
+    };
+    auto load = [&](int t, Stage& st) {
+      t = min(t, t_end - 1);  // past the end: a harmless re-load of the last tile
+      const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
+      const int oy0 = ty0 * Q_H, ox0 = tx0 * PT_W;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int e = ptid + 256 * i;
+        const int px = e >> 3, c4 = (e & 7) * 4;
+        const int py = px / P_W, pxx = px - py * P_W;
+        const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
+        const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
+                        (unsigned)ix < (unsigned)p.w;
+        st.a[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
+      }
+      const __amdgpu_buffer_rsrc_t rd =
+          make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int e = ptid + 256 * i;
+        const int k = e >> 4, c4 = (e & 15) * 4;
+        const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
+        const bool ok = oy < p.oh && ox < p.ow && n0 + c4 < p.N;
+        st.b[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
+      }
+    };
+    auto store = [&](int buf, const Stage& st) {
+      unsigned char* A = smem + buf * Q_STAGE;
+      unsigned char* B = A + 2 * Q_A;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int e = ptid + 256 * i;
+        if (e < EA) {
+          unsigned h0, l0, h1, l1;
+          split2(st.a[i].x, st.a[i].y, h0, l0);
+          split2(st.a[i].z, st.a[i].w, h1, l1);
+          const int o = (e >> 3) * 64 + (e & 7) * 8;
+          *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
+          *reinterpret_cast<u32x2*>(A + Q_A + o) = u32x2{l0, l1};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int e = ptid + 256 * i;
+        unsigned h0, l0, h1, l1;
+        split2(st.b[i].x, st.b[i].y, h0, l0);
+        split2(st.b[i].z, st.b[i].w, h1, l1);
+        const int o = dy64_off(e >> 4, (e & 15) * 4);
+        *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(B + Q_B + o) = u32x2{l0, l1};
+      }
+    };
+    if (n > 0) {  // barriers 1 + n, matching the consumers
+      Stage st;
+      load(t_begin, st);
+      store(0, st);
+      load(t_begin + 1, st);
+      lds_barrier();
+      for (int i = 0;; ++i) {
+        store((i + 1) & 1, st);  // tile i+1 while the consumers multiply tile i
+        load(t_begin + i + 2, st);
+        lds_barrier();
+        if (i + 1 >= n) break;
+      }
+    }
+  } else {  // ----------------------------------------------------------------- consumer
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    if (n > 0) {
+      lds_barrier();
+      for (int t = 0; t < n; ++t) {
+        const unsigned char* A = smem + (t & 1) * Q_STAGE;
+        const unsigned char* B = A + 2 * Q_A;
+        // k-step s: output row 2 rp + (s >> 1), pixels 16 (s & 1) .. +15
+        bf16x8 bh, bl, ah, al, nh, nl;
+        bh = tr_frag_dy64(B, 32 * (2 * rp), 32 * ct, lane);
+        bl = tr_frag_dy64(B + Q_B, 32 * (2 * rp), 32 * ct, lane);
+        pw_frag_pair(A, Q_A, (2 * rp) * P_W, lane, ah, al);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 2 * rp + (s >> 1), px0 = 16 * (s & 1);
+          bf16x8 bh2 = bh, bl2 = bl;
+          if (s < 3) {
+            const int s1 = s + 1, k1 = 32 * (2 * rp + (s1 >> 1)) + 16 * (s1 & 1);
+            bh2 = tr_frag_dy64(B, k1, 32 * ct, lane);
+            bl2 = tr_frag_dy64(B + Q_B, k1, 32 * ct, lane);
+          }
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) {
+            if (tap < 8) {
+              const int t1 = tap + 1;
+              pw_frag_pair(A, Q_A, (row + t1 / 3) * P_W + px0 + t1 % 3, lane, nh, nl);
+            } else if (s < 3) {
+              const int s1 = s + 1;
+              pw_frag_pair(A, Q_A, (2 * rp + (s1 >> 1)) * P_W + 16 * (s1 & 1), lane, nh, nl);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
+            ah = nh;
+            al = nl;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          bh = bh2;
+          bl = bl2;
+        }
+        lds_barrier();
+      }
+    }
+  }
+  // row pair 1 -> LDS slot of its cout tile; row pair 0 adds it in place ((rp 0) + (rp 1)); then
+  // all 512 threads store both cout tiles (deterministic)
+  constexpr int SLOT = 9 * 16 * 64;  // floats: tile t, register r, lane
+  static_assert(2 * SLOT * 4 <= 2 * Q_STAGE, "reduction slots fit the staging LDS");
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();  // the last tile's LDS reads are done
+  if (wave < 4 && rp == 1) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[ct * SLOT + (t * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (wave < 4 && rp == 0) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float* e = red + ct * SLOT + (t * 16 + r) * 64 + lane;
+        *e = acc[t][r] + *e;
+      }
+  }
+  __syncthreads();
+  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
+  for (int e = threadIdx.x; e < 2 * SLOT; e += 512) {
+    const int c2t = e / SLOT, f = e - c2t * SLOT;
+    const int ln = f & 63, r = (f >> 6) & 15, t = f >> 10;
+    const int h = ln >> 5, col = n0 + 32 * c2t + (ln & 31);
+    const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (col >= p.N || ci >= nv) continue;
+    const long m = (long)t * p.C + (s2 ? p.c1 : 0) + cb + ci;
+    float* dst = out + m * p.N + col;
+    *dst = (p.zstride == 0 && p.acc1) ? *dst + red[e] : red[e];
+  }
+}
+
 // ------------------------------------------------------------------------ schedules
 struct Cfg { int bm, bn, tm, tn, occ; };
 // occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
@@ -1634,14 +1824,22 @@ extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p) {
          p->c1 % 16 == 0 && p->c2 % 16 == 0 && p->N % 4 == 0 && p->pt >= 0 && p->pt <= 2 &&
          p->pl >= 0 && p->pl <= 2;
 }
-extern "C" int pld__x3_patch_wgrad_tiles(const GemmConvParams* p) {
-  return (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, x3::PT_H) * p->n);
-}
 // output channels per workgroup of the patch WGRAD kernel: 64 (one staged patch feeds two
 // 32-wide cout tiles) where that pads no more MFMA columns than 32-wide tiles do (N = 240: 256
 // either way, dec1 wgrad 0.66 -> 0.56 ms); N = 144 keeps 32 (192 vs 160 padded: no gain)
 extern "C" int pld__x3_patch_wgrad_cw(int N) {
   return (N > 32 && 2 * cdiv(N, 64) == cdiv(N, 32)) ? 64 : 32;
+}
+// output rows per tile: 8, or 4 for the double-buffered 64-cout kernel
+extern "C" int pld__x3_patch_wgrad_th(int N) {
+#ifdef X3_PW64_SINGLE  // the round-2 single-stage 64-cout kernel (A/B builds only)
+  return x3::PT_H;
+#else
+  return pld__x3_patch_wgrad_cw(N) == 64 ? x3::Q_H : x3::PT_H;
+#endif
+}
+extern "C" int pld__x3_patch_wgrad_tiles(const GemmConvParams* p) {
+  return (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, pld__x3_patch_wgrad_th(p->N)) * p->n);
 }
 
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream) {
@@ -1655,8 +1853,13 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
   const int chunks = p->kc1 + (int)cdiv(p->c2, 32);
   if (pld__x3_patch_wgrad_cw(p->N) == 64) {
     dim3 grid(chunks, cdiv(p->N, 64), cdiv(tiles, tps));
+#ifdef X3_PW64_SINGLE
     x3::conv_x3_patch_wgrad64_kernel<<<grid, x3::PW64_T, 0, as_stream(stream)>>>(*p, tiles, tps);
     return check_launch("conv_x3_patch_wgrad64_kernel");
+#else
+    x3::conv_x3_patch_wgrad64_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
+    return check_launch("conv_x3_patch_wgrad64_pc_kernel");
+#endif
   }
   dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
 #ifdef X3_PW_UNIFORM  // the round-2 uniform-role kernel (A/B builds only)

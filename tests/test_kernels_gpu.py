@@ -217,7 +217,10 @@ def test_conv_dgrad_strided_1x1(cuda, math, n, h, w, c, cout):
                                   (2, 11, 35, 48, 24, 3, 1, 32, True),
                                   # the 64-cout patch WGRAD (dec1-like: concat of 32-channel
                                   # chunks with a ragged 16-channel one, N = 240, 28 x 28)
-                                  (2, 28, 28, 64, 48, 3, 1, 240, False)])
+                                  (2, 28, 28, 64, 48, 3, 1, 240, False),
+                                  # its 4-row tiles with ragged rows, columns and a ragged
+                                  # second cout tile (N = 112: 64 + 48)
+                                  (1, 15, 37, 32, 16, 3, 1, 112, False)])
 def test_conv_every_schedule(cuda, case, math):
     """Each tile x split-K schedule computes the same conv (fwd with bias routing, dgrad into
     two concat destinations with accumulate)."""
