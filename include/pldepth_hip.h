@@ -270,6 +270,12 @@ int pld_bn_add_bwd(const float* x, const float* dy, int64_t rows, int c, const f
 int pld_bn_inference_coeffs(const float* gamma, const float* beta, const float* moving_mean,
                             const float* moving_var, int c, float eps, float* scale, float* shift,
                             void* stream);
+/* training-mode BN as a per-channel affine map of its input, from the batch statistics:
+ * scale = gamma*invstd, shift = beta - mean*scale (the conv input prologue: the consuming conv
+ * applies act(x*scale + shift) while staging its operand, so the BN output is never
+ * materialised; replaces the FusedBatchNormV3 output write + the next Conv2D's read of it) */
+int pld_bn_train_coeffs(const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, int c, float* scale, float* shift, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Elementwise / resampling

@@ -94,6 +94,7 @@ _SIGS = {
     "pld_scale_per_sample": (I32, [P, P, I32, I64, P, I32, P]),
     "pld_dropconnect_scales": (I32, [P, I32, F32, U64, U64, I32, I32, P]),
     "pld_bn_inference_coeffs": (I32, [P, P, P, P, I32, F32, P, P, P]),
+    "pld_bn_train_coeffs": (I32, [P, P, P, P, I32, P, P, P]),
     "pld_dwconv_fwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
     "pld_dwconv_fwd_bn": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P, P,
                                 P, I32, P, P]),

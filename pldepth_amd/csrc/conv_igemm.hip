@@ -827,9 +827,9 @@ constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
 
-// bf16x3 eligibility: channel counts (vector staging) and no fused input prologue
+// bf16x3 eligibility: channel counts (vector staging); a fused input prologue on one source only
 static bool x3_fwd_geom(int C, int c1, bool prologue, int taps) {
-  return C % 8 == 0 && c1 % 8 == 0 && !prologue && taps <= 32;
+  return C % 8 == 0 && c1 % 8 == 0 && (!prologue || c1 == C) && taps <= 32;
 }
 
 // Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), [2 n3,
@@ -971,7 +971,8 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   }
   if (x3) {
     PLD_CHECK_ARG(aligned16(p.x1) && (!p.x2 || aligned16(p.x2)) && aligned16(p.bmat) &&
-                      (!p.bsplit || aligned16(p.bsplit)),
+                      (!p.bsplit || aligned16(p.bsplit)) &&
+                      (!p.in_scale || (aligned16(p.in_scale) && aligned16(p.in_shift))),
                   "%s: bf16x3 operands must be 16-byte aligned", who);
     if (!p.bsplit) {  // the kernel stages a pre-split filter: split into the workspace's tail
       const size_t sb = x3_split_bytes(p.N, p.K);

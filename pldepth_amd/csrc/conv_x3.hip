@@ -25,8 +25,9 @@
 //   FWD/DGRAD staging: full 128-byte lines — 8 lanes per row, 4 consecutive k (channels of one
 //     tap and one source, since C % 8 == 0) per lane; the filter operand is pre-split
 //     (pld_filter_split; the host splits into the workspace when the caller has no copy) and
-//     staged as-is. The fused input prologue is not supported here (those convs take the fp32
-//     kernel).
+//     staged as-is. A one-source FWD conv may carry the fused input prologue act(x*s[c] + t[c])
+//     (the BatchNorm apply + activation of the layer that produced x, never materialised): the
+//     producers apply it to in-image elements between the global load and the split (PRO).
 //   WGRAD staging: lanes over 4-channel quads of one pixel (coalesced), stored row-contiguous
 //     into a [k = pixel][channel] image that the consumers read with ds_read_b64_tr_b16
 //     (hardware transpose) into the k-contiguous MFMA fragments.
@@ -131,7 +132,7 @@ struct X3Smem {
 // the same, unconditional set of loads (the concat's second source is a template parameter, the
 // last steps re-fetch the final tile), so the compiler can count the loads in flight and wait
 // for exactly one stage (vmcnt(N)), never draining the prefetch (vmcnt(0)).
-template <int BM, int BN, int MODE, bool CAT, bool TI>
+template <int BM, int BN, int MODE, bool CAT, bool TI, bool PRO>
 __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned char* smem,
                                             int kt_begin, int kt_end, int pw, int lane, int mb,
                                             int nb) {
@@ -235,7 +236,10 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
   constexpr int RB = (MODE == MODE_FWD) ? FB : 4 * PB;  // and B
   struct Stage {  // one K-step in flight
     float4 ra[RA], rb[RB];
+    float4 ps, pt;  // PRO: this lane's 4 channels' prologue scale / shift
+    unsigned okm;   // PRO: bit j = A row j's element lies inside the image (else it stays 0)
   };
+  static_assert(!PRO || (MODE == MODE_FWD && !CAT), "prologue: one-source FWD view only");
 
   auto load_tile = [&](int kt, Stage& st) {
     const int k0 = kt * BK;
@@ -253,10 +257,18 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       const bool kin = c < cs;
       const int ty = (int)p.dKW.div((uint32_t)tap);
       const int toff = ty * p.w + (tap - ty * p.kw);  // pixel offset of the tap
+      unsigned okm = 0;
 #pragma unroll
       for (int j = 0; j < FA; ++j) {
         const bool ok = kin && ((a_taps[j] >> tap) & 1u);
+        okm |= (unsigned)ok << j;
         st.ra[j] = bload4(rs, ok ? (unsigned)(((a_base[j] + toff) * cs + c) * 4) : OOB);
+      }
+      if constexpr (PRO) {  // unconditional loads (clamped channel): no branch around them
+        const int cc = kin ? c : 0;
+        st.ps = *reinterpret_cast<const float4*>(p.in_scale + cc);
+        st.pt = *reinterpret_cast<const float4*>(p.in_shift + cc);
+        st.okm = okm;
       }
       const int cb8 = chb + 8 * (br & 3);  // this lane's 8-k chunk of the filter
       const int kc = tap * p.C + (s2 ? p.c1 : 0) + cb8;
@@ -275,14 +287,22 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
       const bool src2 = CAT && ci >= p.c1;
       const int cs = src2 ? p.c2 : p.c1;
       const int cb = src2 ? ci - p.c1 : ci;
+      unsigned okm = 0;
 #pragma unroll
       for (int j = 0; j < FA; ++j) {
         const bool ok = kin && ((a_taps[j] >> tap) & 1u);
+        okm |= (unsigned)ok << j;
         const unsigned off = (unsigned)(((a_base[j] + toff) * cs + cb) * 4);
         if (CAT)  // both sources, the other one out of range (reads as 0)
           st.ra[j] = add4(bload4(rs1, (ok && !src2) ? off : OOB), bload4(rs2, (ok && src2) ? off : OOB));
         else
           st.ra[j] = bload4(rs1, ok ? off : OOB);
+      }
+      if constexpr (PRO) {
+        const int cc = kin ? cb : 0;
+        st.ps = *reinterpret_cast<const float4*>(p.in_scale + cc);
+        st.pt = *reinterpret_cast<const float4*>(p.in_shift + cc);
+        st.okm = okm;
       }
       const int kc = k0 + 8 * (br & 3);
       const bool kcin = kc < p.K;
@@ -357,9 +377,13 @@ __device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned ch
 #pragma unroll
       for (int j = 0; j < FA; ++j) {
         const int r = pw * (BM / 4) + 8 * j + lr;
+        float4 v = st.ra[j];
+        if constexpr (PRO)
+          v = ((st.okm >> j) & 1u) ? prologue4(p.in_act, v, st.ps, st.pt)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
         unsigned h0, l0, h1, l1;
-        split2(st.ra[j].x, st.ra[j].y, h0, l0);
-        split2(st.ra[j].z, st.ra[j].w, h1, l1);
+        split2(v.x, v.y, h0, l0);
+        split2(v.z, v.w, h1, l1);
         const int o = chunk_off(r, ks >> 1) + ob;
         *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
         *reinterpret_cast<u32x2*>(A + S::A_PLANE + o) = u32x2{l0, l1};
@@ -482,7 +506,7 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
 // 512 threads: waves 0-3 consume (LDS fragments -> MFMA), waves 4-7 produce the next K-step
 // (global loads, prologue, hi/lo split, LDS stores) — a VALU-heavy wave and an MFMA-heavy
 // wave share each SIMD, so the split overlaps the matrix work.
-template <int BM, int BN, int WM, int WN, int MODE, bool CAT, bool TI>
+template <int BM, int BN, int WM, int WN, int MODE, bool CAT, bool TI, bool PRO = false>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvParams p) {
   static_assert(WM * WN == 4, "4 consumer waves");
   static_assert((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
@@ -508,7 +532,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvPar
     kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
   }
   if (wave >= WM * WN)
-    x3_producer<BM, BN, MODE, CAT, TI>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb, nb);
+    x3_producer<BM, BN, MODE, CAT, TI, PRO>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb,
+                                            nb);
   else
     x3_consumer<BM, BN, WM, WN, MODE>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
 }
@@ -1707,6 +1732,13 @@ template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(GemmConvParams& p, int splits, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
   constexpr int T = (WM * WN + 4) * 64;
+  if constexpr (MODE == MODE_FWD) {
+    if (p.in_scale) {  // one source (x3_fwd_geom)
+      if (p.kc_tap) conv_x3_kernel<BM, BN, WM, WN, MODE, false, true, true><<<grid, T, 0, st>>>(p);
+      else conv_x3_kernel<BM, BN, WM, WN, MODE, false, false, true><<<grid, T, 0, st>>>(p);
+      return;
+    }
+  }
   if (MODE == MODE_FWD && p.kc_tap) {
     if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true, true><<<grid, T, 0, st>>>(p);
     else conv_x3_kernel<BM, BN, WM, WN, MODE, false, true><<<grid, T, 0, st>>>(p);

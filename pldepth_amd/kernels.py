@@ -214,6 +214,12 @@ def conv_args(x1, x2, kh, kw, stride, pad_t, pad_l, oh, ow, cout, in_scale=None,
     return a
 
 
+def conv_kernel_name(args, mode):
+    """The main kernel a conv call with these args launches (pld_conv_kernel_name)."""
+    return lib().pld_conv_kernel_name(C.byref(args), {"fwd": 0, "dgrad": 1, "wgrad": 2}[mode]) \
+        .decode()
+
+
 def filter_to_native(w_hwio, out=None):
     kh, kw, cin, cout = w_hwio.shape
     out = torch.empty((cout, kh, kw, cin), dtype=torch.float32, device=w_hwio.device) \
@@ -660,6 +666,13 @@ def dropconnect_scales(scales, rate, seed, step, layer, image_offset=0):
     else:
         lib().pld_dropconnect_scales(ptr(scales), scales.numel(), float(rate), seed, step, layer,
                                      image_offset, stream())
+
+
+def bn_train_coeffs(mean, invstd, gamma, beta, scale, shift):
+    """Training-mode BN as act-free affine coefficients (scale = gamma*invstd, shift = beta -
+    mean*scale): the consuming conv's input prologue (conv_args in_scale / in_shift)."""
+    lib().pld_bn_train_coeffs(ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), gamma.numel(),
+                              ptr(scale), ptr(shift), stream())
 
 
 def bn_inference_coeffs(gamma, beta, mmean, mvar, scale, shift, eps=1e-3):

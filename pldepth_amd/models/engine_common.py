@@ -71,6 +71,9 @@ class _BN:
         self.invstd = torch.empty(self.c, device=dev)
         self.inf_scale = torch.empty(self.c, device=dev)
         self.inf_shift = torch.empty(self.c, device=dev)
+        # training-mode affine form (train_coeffs): the consuming conv's input prologue
+        self.scale = torch.empty(self.c, device=dev)
+        self.shift = torch.empty(self.c, device=dev)
 
     def stats_(self, x, rows, training):
         if training:
@@ -89,6 +92,12 @@ class _BN:
         else:
             K.conv2d_fwd(args, w_nat, bias, y)
             self.stats_(y, rows, False)
+
+    def train_coeffs(self):
+        """scale = gamma*invstd, shift = beta - mean*scale from this step's batch statistics:
+        a conv that reads the BN input through act(x*scale + shift) (conv_args in_scale /
+        in_shift) never needs the BN output materialised."""
+        K.bn_train_coeffs(self.mean, self.invstd, self.gamma, self.beta, self.scale, self.shift)
 
     def apply(self, x, rows, act, y, training, gate=None, hw=0):
         if training:

@@ -41,6 +41,10 @@ TAPS = ("conv2_block3_out", "conv3_block4_out", "conv4_block3_out", "conv5_block
 # (batch 32, 448x448), with that stage exact it is at the fp32 restatement's own 5e-4;
 # exact stem / conv3-5 stages change nothing measurable. Cost: +1.8 ms per fwd+bwd
 # (36.9 -> 38.7 ms eager; tools/exp_redweb_policy.py, profiles/r03_redweb_policy.txt).
+# Only the FORWARD convs of those stages need it: the activations' rounding is what the chaotic
+# encoder amplifies; the backward's dX convs of the frozen encoder run bf16x3 (their ~2^-16
+# per-product error sits far below the fp32 restatement's own gradient error, ~5e-2 per tensor
+# at batch 32; PLD_REDWEB_EXACT_BWD=1 keeps the backward exact too, for A/B).
 EXACT_STAGES_AUTO = ("conv2",)
 FFLS = [("ffl0", 256, 256, "conv4_block3_out"),
         ("ffl1", 128, 128, "conv3_block4_out"),
@@ -79,6 +83,12 @@ class RedWebFF:
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
+        self.exact_bwd = os.environ.get("PLD_REDWEB_EXACT_BWD", "0") == "1"
+        # encoder bottlenecks in training: conv2 / conv3 read conv1 / conv2's pre-BN output
+        # through the BN + ReLU prologue (their BN outputs are never materialised: the frozen
+        # convs' backward needs no input); PLD_BN_PROLOGUE=0 materialises them (A/B)
+        # (A/B: 1 = both, 2 = conv3 only, 3 = conv2 only)
+        self.bn_prologue = int(os.environ.get("PLD_BN_PROLOGUE", "1"))
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
         self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
         self._side = False
@@ -245,25 +255,32 @@ class RedWebFF:
         return self._gpre[key]
 
     # ------------------------------------------------------------------ forward
-    def _math(self, conv, oh=None, ow=None):
+    def _math(self, conv, oh=None, ow=None, bwd=False):
         if conv.trainable:
             return self.dec_math
-        if self.enc_math == "auto" and conv.name.startswith(self.exact_stages):
+        if (self.enc_math == "auto" and conv.name.startswith(self.exact_stages)
+                and (not bwd or self.exact_bwd)):
             return "fp32"
         # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
         return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
                               getattr(self, "x3_min_population", None))
 
-    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None, bn=None, training=True):
+    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None, bn=None, training=True,
+              pro=None):
         """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout];
-        with `bn`, also that BN's statistics of y (fused into the conv epilogue in training)."""
+        with `bn`, also that BN's statistics of y (fused into the conv epilogue in training);
+        with `pro` (a BN whose train_coeffs are current), the conv reads relu(pro(x))."""
         k, s = conv.k, conv.stride
         if s == 1:
             pt, pl = (k - 1) // 2, (k - 1) // 2
         else:
             pt = pl = 0
-        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
-                           math=self._math(conv, oh, ow))
+        if pro is not None:
+            args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout, pro.scale, pro.shift,
+                               "relu", math=self._math(conv, oh, ow))
+        else:
+            args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
+                               math=self._math(conv, oh, ow))
         if bn is not None:
             assert not acc and x2 is None
             bn.conv_fwd_stats(args, conv.w_nat, conv.b, y, self.B * oh * ow, training)
@@ -311,14 +328,41 @@ class RedWebFF:
         else:
             sc = x
         self._conv(blk["c1"], x, A[n + "1_pre"], h, w, oh, ow, bn=blk["bn1"], training=training)
-        blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
-        self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
-                   bn=blk["bn2"], training=training)
-        blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
-        self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
-                   bn=blk["bn3"], training=training)
+        if training and self.bn_prologue:
+            # conv2 reads 1_pre through bn1 + ReLU; conv3 reads 2_pre through bn2 + ReLU unless
+            # its 1x1 GEMM runs on the streaming wide kernel (no prologue there): then 2_relu
+            if self.bn_prologue in (1, 3):
+                blk["bn1"].train_coeffs()
+                self._conv(blk["c2"], A[n + "1_pre"], A[n + "2_pre"], oh, ow, oh, ow,
+                           bn=blk["bn2"], training=training, pro=blk["bn1"])
+            else:
+                blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
+                self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
+                           bn=blk["bn2"], training=training)
+            if self.bn_prologue == 3 or self._wide(blk["c3"], A[n + "2_pre"], oh, ow):
+                blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
+                self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
+                           bn=blk["bn3"], training=training)
+            else:
+                blk["bn2"].train_coeffs()
+                self._conv(blk["c3"], A[n + "2_pre"], A[n + "3_pre"], oh, ow, oh, ow,
+                           bn=blk["bn3"], training=training, pro=blk["bn2"])
+        else:
+            blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
+            self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
+                       bn=blk["bn2"], training=training)
+            blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
+            self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
+                       bn=blk["bn3"], training=training)
         blk["bn3"].add_apply(A[n + "3_pre"], rows, sc, "relu", A[n + "out"], training)
         return A[n + "out"]
+
+    def _wide(self, conv, x, h, w):
+        """Whether this stride-1 1x1 conv's forward runs on the streaming wide / thin kernels
+        (which take no input prologue)."""
+        args = K.conv_args(x, None, conv.k, conv.k, 1, 0, 0, h, w, conv.cout,
+                           math=self._math(conv, h, w))
+        return K.conv_kernel_name(args, "fwd") in ("wide1x1_kernel", "thin1x1_kernel")
 
     def _bottleneck_fwd(self, bt, x, h, w, training):
         A, n = self.act, bt["name"]
@@ -371,7 +415,7 @@ class RedWebFF:
         k, s = conv.k, conv.stride
         pt = pl = ((k - 1) // 2 if s == 1 else 0)
         args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout,
-                           math=self._math(conv, oh, ow))
+                           math=self._math(conv, oh, ow, bwd=True))
         if conv.trainable:
             if self._side:
                 def wg(args=args, gy=gy, rows=self.B * oh * ow, conv=conv):

@@ -270,6 +270,59 @@ def test_conv_every_schedule(cuda, case, math):
                                       torch.empty(n, h, w, cout, device=cuda).data_ptr(), 0, None)
 
 
+@pytest.mark.parametrize("math", MATHS)
+@pytest.mark.parametrize("case", [(2, 14, 12, 64, 3, 96, "relu"), (1, 9, 11, 256, 1, 64, "relu"),
+                                  (2, 10, 9, 32, 3, 48, "swish"), (2, 7, 9, 128, 3, 130, "relu"),
+                                  (3, 5, 7, 512, 1, 200, "none")])
+def test_conv_prologue_every_schedule(cuda, case, math):
+    """The fused input prologue y = conv(act(x*scale + shift)) (a BatchNorm apply + activation
+    of the producing layer, never materialised) on every schedule of a one-source conv: padding
+    taps stay zero after the activation (they are not act(shift)); tap-inner (3x3, C >= 64),
+    linear (3x3 on 32 channels) and 1x1 K orders, ragged M and N tiles."""
+    n, h, w, c, k, cout, act = case
+    torch.manual_seed(c + cout)
+    x = torch.randn(n, h, w, c, dtype=torch.float64)
+    wt = torch.randn(k, k, c, cout, dtype=torch.float64) / np.sqrt(k * k * c)
+    scale = torch.rand(c, dtype=torch.float64) + 0.5
+    shift = torch.randn(c, dtype=torch.float64) * 0.5
+    z = x * scale + shift
+    a = {"relu": torch.relu(z), "swish": z * torch.sigmoid(z), "none": z}[act]
+    pt, pb, _ = OE.same_pad(h, k, 1)
+    pl, pr, _ = OE.same_pad(w, k, 1)
+    y_ref = OE.conv(a.permute(0, 3, 1, 2), wt, None, 1, (pt, pb, pl, pr)).permute(0, 2, 3, 1)
+    gx, gw = dev(x, cuda), dev(wt, cuda)
+    wn = K.filter_to_native(gw)
+    gsc, gsh = dev(scale, cuda), dev(shift, cuda)
+    tol = CONV_TOL[math]
+    n_sched = _lib.lib().pld_conv_num_schedules(K.MATH[math])
+    for t in list(range(n_sched)) + [-1]:
+        args = K.conv_args(gx, None, k, k, 1, pt, pl, h, w, cout, gsc, gsh, act, math=math)
+        args.tile = t
+        ws = torch.empty(max(_lib.lib().pld_conv2d_fwd_workspace_size(C.byref(args)), 4),
+                         dtype=torch.uint8, device=cuda)
+        args.ws, args.ws_bytes = ws.data_ptr(), ws.numel()
+        y = torch.empty(n, h, w, cout, device=cuda)
+        _lib.lib().pld_conv2d_fwd(C.byref(args), wn.data_ptr(), None, y.data_ptr(), 0, None)
+        torch.cuda.synchronize()
+        assert rel_err(y, y_ref) < tol, (t, rel_err(y, y_ref))
+
+
+def test_bn_train_coeffs(cuda):
+    """scale = gamma*invstd, shift = beta - mean*scale: act(x*scale + shift) == bn_apply."""
+    torch.manual_seed(3)
+    rows, c = 777, 40
+    x = torch.randn(rows, c, device=cuda) * 3 + 1
+    mean, invstd = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_stats(x, rows, c, mean, invstd)
+    gamma, beta = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda)
+    sc, sh = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_train_coeffs(mean, invstd, gamma, beta, sc, sh)
+    y = torch.empty_like(x)
+    K.bn_apply(x, rows, c, mean, invstd, gamma, beta, "relu", y)
+    torch.cuda.synchronize()
+    assert rel_err(torch.relu(x * sc + sh), y) < 1e-6
+
+
 def test_channel_sum(cuda):
     x = torch.randn(1000, 37, dtype=torch.float64)
     out = torch.empty(37, device=cuda)
@@ -772,9 +825,12 @@ def test_maxpool_zero_padded(cuda, shape, relu):
     assert rel_err(dx - 0.5, xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("dres_acc", [True, False])
 @pytest.mark.parametrize("rows,c,act", [(3000, 64, "relu"), (517, 256, "none"),
-                                        (200, 6, "relu")])
-def test_bn_add_forward_backward(cuda, rows, c, act):
+                                        (200, 6, "relu"), (4099, 128, "relu")])
+def test_bn_add_forward_backward(cuda, rows, c, act, dres_acc):
+    """pld_bn_add_apply / pld_bn_add_bwd vs autograd; a fresh dres with an activation takes the
+    dz-storing reduction pass (the elementwise pass then reads (x, dz))."""
     from oracle import redweb as OR
     torch.manual_seed(rows + c)
     x = torch.randn(rows, c, dtype=torch.float64) * 2 + 0.5
@@ -794,14 +850,15 @@ def test_bn_add_forward_backward(cuda, rows, c, act):
     gres, ggam, gbet = dev(res, cuda), dev(gamma, cuda), dev(beta, cuda)
     K.bn_add_apply(gx, rows, c, gm, gi, ggam, gbet, gres, act, y)
     dx = torch.empty_like(gx)
+    base = 2.0 if dres_acc else 0.0
     dres = torch.full_like(gx, 2.0)
     dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
     K.bn_add_bwd(gx, dev(dy, cuda), rows, c, gm, gi, ggam, gbet, gres, act, dx, dres, dg, db,
-                 dres_accumulate=True)
+                 dres_accumulate=dres_acc)
     torch.cuda.synchronize()
     assert rel_err(y, y_ref) < 1e-5
     assert rel_err(dx, xr.grad) < 1e-4
-    assert rel_err(dres - 2.0, rr.grad) < 1e-5
+    assert rel_err(dres - base, rr.grad) < 1e-5
     assert rel_err(dg, gr.grad) < 1e-5
     assert rel_err(db, br.grad) < 1e-5
 

@@ -16,11 +16,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def a_pro(args):
+    return bool(args.in_scale)
+
+
 def timed_step(tr, lr):
     from pldepth_amd import kernels as K
     st = tr.stream
     recs = []
-    orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad")}
+    orig = {n: getattr(K, n) for n in ("conv2d_fwd", "conv2d_dgrad", "conv2d_wgrad",
+                                       "conv2d_fwd_bn_stats")}
 
     def wrap(name):
         fn = orig[name]
@@ -31,7 +36,9 @@ def timed_step(tr, lr):
             r = fn(args, *rest, **kw)
             e1.record(st)
             mode = name.split("_")[1]
-            if mode == "fwd":
+            if a_pro(args):
+                mode += "+p"
+            if mode.startswith("fwd"):
                 M, N, Kd = args.n * args.oh * args.ow, args.cout, args.kh * args.kw * (args.c1 + args.c2)
             elif mode == "dgrad":
                 M, N, Kd = args.n * args.h * args.w, args.c1 + args.c2, args.kh * args.kw * args.cout
