@@ -227,7 +227,21 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ part,
   __shared__ double rs[4], rq[4];
   const double2* run = reinterpret_cast<const double2*>(part) + (long)c * nbx;
   double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < nbx; i += 256) {
+  // U partials in flight per thread per trip (a GEMM epilogue leaves up to M/32 partials per
+  // channel: 12544 at 112^2 x 32, i.e. 49 dependent round trips per thread one at a time)
+  constexpr int U = 8;
+  int i = threadIdx.x;
+  for (; i + (U - 1) * 256 < nbx; i += U * 256) {
+    double2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = run[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a += v[u].x;
+      b += v[u].y;
+    }
+  }
+  for (; i < nbx; i += 256) {
     const double2 v = run[i];
     a += v.x;
     b += v.y;

@@ -1725,6 +1725,9 @@ static const Cfg kCfg[] = {
     {256, 32, 2, 1, 2},  {128, 64, 2, 1, 3},  {128, 96, 1, 3, 2},  {128, 128, 2, 2, 2},
     {128, 160, 1, 5, 2}, {128, 192, 1, 6, 1}, {128, 224, 1, 7, 1}, {256, 64, 2, 2, 1},
     {256, 128, 4, 2, 1}, {128, 256, 2, 4, 1},
+    // short-M / long-K launches (the encoder's 14x14 and 28x28 1x1 convs at batch 32: 147-294
+    // tiles of 128 x 64 leave most of the 256 CUs idle): 4x the workgroups, 4 resident per CU
+    {64, 64, 1, 1, 4},
 };
 constexpr int kNumCfg = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
 
@@ -1760,7 +1763,8 @@ static void launch(GemmConvParams& p, int splits, int cfg, hipStream_t st) {
     case 6: launch_cfg<MODE, 128, 224, 4, 1>(p, splits, st); break;
     case 7: launch_cfg<MODE, 256, 64, 4, 1>(p, splits, st); break;
     case 8: launch_cfg<MODE, 256, 128, 2, 2>(p, splits, st); break;
-    default: launch_cfg<MODE, 128, 256, 2, 2>(p, splits, st); break;
+    case 9: launch_cfg<MODE, 128, 256, 2, 2>(p, splits, st); break;
+    default: launch_cfg<MODE, 64, 64, 2, 2>(p, splits, st); break;
   }
 }
 

@@ -50,42 +50,48 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = p.K, LA = K + 4;
   float* sa = smem;                       // [64][LA]; after the MACs: [4][64][NW + 4] outputs
-  constexpr int PG_MAXQ = MQ;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long m0 = (long)blockIdx.x * 64;
   const int rows = (int)min(64L, (long)p.M - m0);
-  const int kq = K / 4, nv = rows * kq, NV = 64 * kq;
+  // a thread owns ONE channel quad q of rows r0, r0 + rpp, ... (rpp = 256 / (K/4) rows per pass,
+  // each pass a contiguous run of rpp rows): the BN coefficients of its quad are loaded once,
+  // not once per element (bn_apply_kernel's scheme); every load is in flight before any is used
+  const int kq = K / 4, rpp = 256 / kq;
+  const int q = tid % kq, r0 = tid / kq, c = 4 * q;
+  const bool act_t = r0 < rpp;
   const float4* s1 = reinterpret_cast<const float4*>(p.x + m0 * K);
   const float4* s2 = reinterpret_cast<const float4*>((PRO == PRO_BNBWD ? p.dy : p.x) + m0 * K);
-  // loads first (all in flight), then the prologue and the LDS stores
-  float4 va[PG_MAXQ], vb[PG_MAXQ];
+  float4 va[MQ], vb[MQ];
 #pragma unroll
-  for (int j = 0; j < PG_MAXQ; ++j) {
-    const int e = tid + 256 * j;
-    va[j] = vb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < nv) {
-      va[j] = s1[e];
-      if (PRO == PRO_BNBWD) vb[j] = s2[e];
-    }
+  for (int j = 0; j < MQ; ++j) {  // clamped, unconditional loads (rows past the tile: zeroed)
+    const int r = min(r0 + j * rpp, rows - 1);
+    va[j] = s1[r * kq + q];
+    if (PRO == PRO_BNBWD) vb[j] = s2[r * kq + q];
+  }
+  const float4 mu4 = *reinterpret_cast<const float4*>(p.mean + c);
+  const float4 is4 = *reinterpret_cast<const float4*>(p.invstd + c);
+  const float4 ga4 = *reinterpret_cast<const float4*>(p.gamma + c);
+  const float4 be4 = *reinterpret_cast<const float4*>(p.beta + c);
+  const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+  const float ga[4] = {ga4.x, ga4.y, ga4.z, ga4.w}, be[4] = {be4.x, be4.y, be4.z, be4.w};
+  float k1[4] = {0.f, 0.f, 0.f, 0.f}, k2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (PRO == PRO_BNBWD) {
+    const float4 k14 = *reinterpret_cast<const float4*>(p.k12 + c);
+    const float4 k24 = *reinterpret_cast<const float4*>(p.k12 + K + c);
+    k1[0] = k14.x; k1[1] = k14.y; k1[2] = k14.z; k1[3] = k14.w;
+    k2[0] = k24.x; k2[1] = k24.y; k2[2] = k24.z; k2[3] = k24.w;
   }
 #pragma unroll
-  for (int j = 0; j < PG_MAXQ; ++j) {
-    const int e = tid + 256 * j;
-    if (e >= NV) break;
-    const int r = e / kq, c = 4 * (e - r * kq);
+  for (int j = 0; j < MQ; ++j) {
+    const int r = r0 + j * rpp;
+    if (!act_t || r >= 64) break;
     const float xs[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
     const float ds[4] = {vb[j].x, vb[j].y, vb[j].z, vb[j].w};
-    const float4 mu4 = *reinterpret_cast<const float4*>(p.mean + c);
-    const float4 is4 = *reinterpret_cast<const float4*>(p.invstd + c);
-    const float4 ga4 = *reinterpret_cast<const float4*>(p.gamma + c);
-    const float4 be4 = *reinterpret_cast<const float4*>(p.beta + c);
-    const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
-    const float ga[4] = {ga4.x, ga4.y, ga4.z, ga4.w}, be[4] = {be4.x, be4.y, be4.z, be4.w};
     float o[4];
     if (PRO == PRO_BNACT) {
       float g[4] = {1.f, 1.f, 1.f, 1.f};
-      if (p.gate && e < nv) {
+      if (p.gate && r < rows) {
         const long img = (long)p.dHW.div((uint32_t)(m0 + r));
         const float4 g4 = *reinterpret_cast<const float4*>(p.gate + img * K + c);
         g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
@@ -94,9 +100,6 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgParams p) {
       for (int u = 0; u < 4; ++u)  // bn_apply_kernel's arithmetic (then act, then the gate)
         o[u] = act_fwd(p.act, ((xs[u] - mu[u]) * is[u]) * ga[u] + be[u]) * g[u];
     } else {
-      const float4 k14 = *reinterpret_cast<const float4*>(p.k12 + c);
-      const float4 k24 = *reinterpret_cast<const float4*>(p.k12 + K + c);
-      const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {  // bn_bwd_apply_kernel's arithmetic
         const float xh = (xs[u] - mu[u]) * is[u];
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgParams p) {
         o[u] = (is[u] * ga[u]) * (dz - k1[u] - xh * k2[u]);
       }
     }
-    if (e >= nv) o[0] = o[1] = o[2] = o[3] = 0.f;
+    if (r >= rows) o[0] = o[1] = o[2] = o[3] = 0.f;
     *reinterpret_cast<float4*>(sa + r * LA + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
@@ -178,7 +181,7 @@ static int pg_launch(PgParams& p, int pro, hipStream_t st) {
   const int nw = (p.N + 3) / 4;
   const size_t lds = sizeof(float) * std::max(64 * (p.K + 4), 4 * 64 * (12 + 4));
   const unsigned grid = cdiv(p.M, 64);
-  const int mq = (p.K + 15) / 16;
+  const int mq = (int)cdiv(64, 256 / (p.K / 4));  // passes of rpp rows per thread
 #define PG3(NWV, MQV)                                                                      \
   if (pro == PRO_BNACT) pgemm_kernel<PRO_BNACT, NWV, MQV><<<grid, 256, lds, st>>>(p);      \
   else pgemm_kernel<PRO_BNBWD, NWV, MQV><<<grid, 256, lds, st>>>(p);
@@ -186,7 +189,7 @@ static int pg_launch(PgParams& p, int pro, hipStream_t st) {
   if (mq <= 4) { PG3(NWV, 4) }                     \
   else if (mq <= 8) { PG3(NWV, 8) }                \
   else if (mq <= 12) { PG3(NWV, 12) }              \
-  else { PG3(NWV, 15) }
+  else { PG3(NWV, 16) }
   if (nw <= 4) { PG(4) }
   else if (nw <= 6) { PG(6) }
   else if (nw <= 10) { PG(10) }

@@ -84,11 +84,14 @@ class RedWebFF:
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
         self.exact_bwd = os.environ.get("PLD_REDWEB_EXACT_BWD", "0") == "1"
-        # encoder bottlenecks in training: conv2 / conv3 read conv1 / conv2's pre-BN output
-        # through the BN + ReLU prologue (their BN outputs are never materialised: the frozen
-        # convs' backward needs no input); PLD_BN_PROLOGUE=0 materialises them (A/B)
-        # (A/B: 1 = both, 2 = conv3 only, 3 = conv2 only)
-        self.bn_prologue = int(os.environ.get("PLD_BN_PROLOGUE", "1"))
+        # PLD_BN_PROLOGUE (A/B, default 0): encoder bottlenecks in training read conv1 / conv2's
+        # pre-BN output through the BN + ReLU input prologue of the next conv (1 = conv2 and
+        # conv3, 2 = conv3 only, 3 = conv2 only), so those BN outputs are never materialised.
+        # Measured on MI355X (profiles/r03_prologue_ab.txt): it removes 0.5 ms of bn_apply per
+        # step but the prologue'd bf16x3 convs run 0.9 ms slower (the conv kernel is issue- and
+        # latency-bound: ~30 % per launch for 2 loads + 8 FMAs per staged float4), 873 -> 863
+        # img/s; so the BN outputs stay materialised.
+        self.bn_prologue = int(os.environ.get("PLD_BN_PROLOGUE", "0"))
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
         self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
         self._side = False
