@@ -252,6 +252,27 @@ def attach_traffic(roof, path, workload):
     roof["traffic_over_algorithmic"] = t["hbm_over_algorithmic"]
 
 
+def attach_graph_frac(roof, path, workload):
+    """The dominant kernel's fraction of peak as rocprof measured it in graph replay (the timed
+    steps' own execution: the decoder weight gradients then overlap the encoder backward on a
+    side stream), from the kernel-trace summary committed at the same HEAD and workload; the
+    top-level frac stays the HIP-event figure of this run's eager profiling step."""
+    if path and not os.path.isabs(path):
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), path)
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return
+    d = roof.get("dominant", {})
+    if t.get("kernel") != roof["kernel"] or t.get("workload") != workload or \
+            t.get("launches_per_step") != d.get("launches_per_step"):
+        return
+    ach = d["flops_per_step"] / (t["ms_per_step"] * 1e-3) / 1e12
+    roof["graph_replay"] = {"ms_per_step": t["ms_per_step"], "achieved": round(ach, 3),
+                            "frac": round(ach / roof["peak"], 4), "source": t["source"]}
+
+
 def conv_roofline(recs, traffic_profile=None):
     """roofline object. Top level = the DOMINANT kernel (the conv kernel name with the largest
     summed time in the profiled step): achieved = its algorithmic FLOPs / its measured time, peak
@@ -524,10 +545,12 @@ def main():
                     help="conv arithmetic policy (kernels.conv_policy): auto = decoder bf16x3, "
                          "encoder bf16x3 where the BN sees >= 4096 values per channel (all of "
                          "them at 448x448 batch 32); mixed = encoder fp32, decoder bf16x3")
-    ap.add_argument("--traffic-profile", default="profiles/r02_pmc_dominant.json",
+    ap.add_argument("--traffic-profile", default="profiles/r03_pmc_dominant.json",
                     help="PMC traffic of the dominant kernel (tools/dominant_traffic.py, committed "
                          "from the same HEAD and workload): fills roofline.traffic when its kernel "
                          "and workload match this run's")
+    ap.add_argument("--graph-profile", default="profiles/r03_dominant_graph.json",
+                    help="rocprof graph-replay time of the dominant kernel (roofline.graph_replay)")
     ap.add_argument("--step-traffic-profile", default="profiles/r03_pmc_step_family.json",
                     help="PMC HBM bytes of one eager step per op family "
                          "(tools/pmc_step_family.py): roofline.step_bytes_measured")
@@ -583,6 +606,7 @@ def main():
         "definition": "per launch, every distinct tensor the call is handed counted once (inputs "
                       "read once, outputs written once), summed over one step's launches"}
     attach_step_traffic(roof, a.step_traffic_profile, workload)
+    attach_graph_frac(roof, a.graph_profile, workload)
     out = {
         "metric": "images/sec (448x448, ranking_size=5) at 1/2/4/8 GPU; ListMLE loss delta vs TF2",
         "value": round(value, 3),
