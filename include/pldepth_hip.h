@@ -280,6 +280,12 @@ int pld_bn_train_coeffs(const float* mean, const float* invstd, const float* gam
 /* ------------------------------------------------------------------------------------------
  * Elementwise / resampling
  * ------------------------------------------------------------------------------------------ */
+/* y[r][0..cin) = x[r][c]*scale[c] + shift[c] (scale/shift NULL: identity), y[r][cin..cout) = 0,
+ * cout = 4 or 8: a 3-channel network input widened for the stem conv's vector / bf16x3 kernels
+ * (TF zero-pads the normalised map, so padding taps stay zero either way); replaces the
+ * Rescaling + Normalization (EfficientNetB0) of the input before its stem Conv2D */
+int pld_channel_pad_affine(const float* x, int64_t rows, int cin, int cout, const float* scale,
+                           const float* shift, float* y, void* stream);
 /* y = act(x*scale[c] + shift[c]) (input normalisation, bias+act) over [rows][c] */
 int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
                            const float* shift, int act, float* y, void* stream);

@@ -95,6 +95,7 @@ _SIGS = {
     "pld_dropconnect_scales": (I32, [P, I32, F32, U64, U64, I32, I32, P]),
     "pld_bn_inference_coeffs": (I32, [P, P, P, P, I32, F32, P, P, P]),
     "pld_bn_train_coeffs": (I32, [P, P, P, P, I32, P, P, P]),
+    "pld_channel_pad_affine": (I32, [P, I64, I32, I32, P, P, P, P]),
     "pld_dwconv_fwd": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
     "pld_dwconv_fwd_bn": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, P, P, P,
                                 P, I32, P, P]),

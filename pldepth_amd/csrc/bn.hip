@@ -499,9 +499,45 @@ __global__ void bn_train_coeffs_kernel(const float* __restrict__ mean,
   sh[i] = b[i] - mean[i] * s;
 }
 
+// one output row (cout = 4 or 8 floats: 1 or 2 float4) per thread
+template <int CO>
+__global__ __launch_bounds__(256) void channel_pad_affine_kernel(
+    const float* __restrict__ x, long rows, int cin, const float* __restrict__ sc,
+    const float* __restrict__ sh, float* __restrict__ y) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float o[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    float v = 0.f;
+    if (c < cin) {
+      v = x[r * cin + c];
+      if (sc) v = v * sc[c] + sh[c];
+    }
+    o[c] = v;
+  }
+  float4* d = reinterpret_cast<float4*>(y + r * CO);
+#pragma unroll
+  for (int q = 0; q < CO / 4; ++q) d[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+}
+
 }  // namespace pld
 
 using namespace pld;
+
+extern "C" int pld_channel_pad_affine(const float* x, int64_t rows, int cin, int cout,
+                                      const float* scale, const float* shift, float* y,
+                                      void* stream) {
+  PLD_CHECK_ARG(x && y && rows > 0 && cin > 0 && cin <= cout && (cout == 4 || cout == 8) &&
+                    aligned16(y) && (scale == nullptr) == (shift == nullptr),
+                "pld_channel_pad_affine: bad args");
+  const unsigned g = (unsigned)cdiv(rows, 256);
+  if (cout == 4)
+    channel_pad_affine_kernel<4><<<g, 256, 0, as_stream(stream)>>>(x, rows, cin, scale, shift, y);
+  else
+    channel_pad_affine_kernel<8><<<g, 256, 0, as_stream(stream)>>>(x, rows, cin, scale, shift, y);
+  return check_launch("channel_pad_affine_kernel");
+}
 
 extern "C" int pld_bn_train_coeffs(const float* mean, const float* invstd, const float* gamma,
                                    const float* beta, int c, float* scale, float* shift,

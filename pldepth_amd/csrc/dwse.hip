@@ -427,6 +427,18 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
       ga = *reinterpret_cast<const float4*>(pr.gamma + 4 * q);
       be = *reinterpret_cast<const float4*>(pr.beta + 4 * q);
     }
+    // BNB: act and act' from ONE sigmoid for swish (act_fwd and act_grad each evaluated it: two
+    // exp + two rcp per element, which the compiler did not merge across the runtime switch)
+    auto act2 = [&](float z, float& av, float& ag) {
+      if (pr.act == ACT_SWISH) {
+        const float sg = sigmoidf_(z);
+        av = z * sg;
+        ag = sg * (1.f + z * (1.f - sg));
+      } else {
+        av = act_fwd(pr.act, z);
+        ag = act_grad(pr.act, z);
+      }
+    };
     auto acc1 = [&](float4 v, float4 u) {
       if constexpr (BNB) {
         const float xs[4] = {v.x, v.y, v.z, v.w}, us[4] = {u.x, u.y, u.z, u.w};
@@ -436,7 +448,8 @@ __global__ __launch_bounds__(256) void img_chan_sum_kernel(const float* __restri
         for (int e = 0; e < 4; ++e) {
           const float xh = (xs[e] - mus[e]) * iss[e];
           const float z = xh * gas[e] + bes[e];
-          const float av = act_fwd(pr.act, z), ag = act_grad(pr.act, z);
+          float av, ag;
+          act2(z, av, ag);
           const float dg = us[e] * ag;
           s[e] += (double)(av * us[e]);
           bs[0][e] += (double)dg;

@@ -675,6 +675,14 @@ def bn_train_coeffs(mean, invstd, gamma, beta, scale, shift):
                               ptr(scale), ptr(shift), stream())
 
 
+def channel_pad_affine(x, cout, y, scale=None, shift=None):
+    """y [.., cout] = [x*scale + shift | 0] of x [.., cin] (the stem's widened input)."""
+    cin = x.shape[-1]
+    lib().pld_channel_pad_affine(ptr(x), x.numel() // cin, cin, cout, ptr(scale), ptr(shift),
+                                 ptr(y), stream())
+    return y
+
+
 def bn_inference_coeffs(gamma, beta, mmean, mvar, scale, shift, eps=1e-3):
     lib().pld_bn_inference_coeffs(ptr(gamma), ptr(beta), ptr(mmean), ptr(mvar), gamma.numel(),
                                   eps, ptr(scale), ptr(shift), stream())

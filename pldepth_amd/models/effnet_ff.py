@@ -115,6 +115,16 @@ class EffNetFF:
             m.bind(self)
         self.norm_scale = torch.empty(3, device=self.device)
         self.norm_shift = torch.empty(3, device=self.device)
+        # PLD_STEM_PAD (A/B, default 0): 4 widens the normalised 3-channel input with zero
+        # channels so the stem conv runs on the vectorised exact-fp32 im2col path (+0.55 % img/s,
+        # profiles/r03_stem_se_ab.txt), but its MFMA k-pairing differs from the 3-channel
+        # path's and, amplified by training-mode BN over 8 values per channel, moves the 64x64
+        # batch-2 top_activation past the 1e-3 test bar (1.13e-3); 0 keeps the scalar path with
+        # the normalisation as its input prologue. The stem stays exact fp32 either way (bf16x3:
+        # 3.8e-3 on the 448x448 prediction at batch 2)
+        self.stem_pad = int(os.environ.get("PLD_STEM_PAD", "0"))
+        if self.stem_pad:
+            self.stem.pad_input_channels(self.stem_pad)
         self.init_weights(seed)
         # thin-N 1x1 convs with the neighbouring BN (+ act, SE gate) folded in (pgemm.hip)
         self.fuse_pgemm = True
@@ -260,6 +270,8 @@ class EffNetFF:
                 self.gact[name] = torch.empty(shape, device=dev)
 
         new("input", (B, H, W, 3), grad=False)
+        if self.stem_pad:
+            new("input_pad", (B, H, W, self.stem_pad), grad=False)
         h, w = H // 2, W // 2
         new("stem_pre", (B, h, w, 32), grad=False)
         new("stem_activation", (B, h, w, 32))
@@ -352,10 +364,19 @@ class EffNetFF:
         pl, _ = correct_pad(self.W, 3)
         x = A["input"]
         h, w = self.H // 2, self.W // 2
-        args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none",
-                 math=self._em(h, w))
         rows = B * h * w
-        self._conv_bn(args, self.stem.w_nat, None, A["stem_pre"], self.stem_bn, rows, training)
+        if self.stem_pad:
+            # the normalised input widened with zero channels: 16-byte rows for the vector path
+            xp = K.channel_pad_affine(x, self.stem_pad, A["input_pad"], self.norm_scale,
+                                      self.norm_shift)
+            args = a(xp, None, 3, 3, 2, pt, pl, h, w, 32, math="fp32")
+            self._conv_bn(args, self.stem.w_pad, None, A["stem_pre"], self.stem_bn, rows,
+                          training)
+        else:
+            args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift,
+                     "none", math=self._em(h, w))
+            self._conv_bn(args, self.stem.w_nat, None, A["stem_pre"], self.stem_bn, rows,
+                          training)
         if training:
             # stem BN + swish applied by block1a's depthwise conv as it reads its taps: the stem
             # activation (its only consumer in training) is never materialised

@@ -170,3 +170,21 @@ class _Conv:
 
     def refresh(self):
         K.filter_refresh(self.w, self.w_nat, self.w_nat_x3, self.w_dg, self.w_dg_x3)
+        if getattr(self, "cpad", 0):
+            self._refresh_padded()
+
+    def pad_input_channels(self, cpad):
+        """Serve this (frozen, input-layer) conv from an input widened to `cpad` channels with
+        zeros (K.channel_pad_affine): a native filter with zero taps for the extra channels
+        (+ its bf16x3 split when cpad % 8 == 0), rebuilt by refresh()."""
+        self.cpad = cpad
+        self.w_pad = torch.empty(self.cout, self.k, self.k, cpad, device=self.w.device)
+        self.w_pad_x3 = torch.empty_like(self.w_pad) if cpad % 8 == 0 else None
+        self._refresh_padded()
+
+    def _refresh_padded(self):
+        wp = torch.zeros(self.k, self.k, self.cpad, self.cout, device=self.w.device)
+        wp[:, :, :self.cin, :] = self.w  # layout plumbing, once per weight load
+        K.filter_to_native(wp, self.w_pad)
+        if self.w_pad_x3 is not None:
+            K.filter_split(self.w_pad, self.w_pad_x3)

@@ -78,6 +78,12 @@ class RedWebFF:
         self.stats.materialize(self.device)
         for m in self.bns + self.convs:
             m.bind(self)
+        # PLD_STEM_PAD (A/B, default 0): the 3-channel input widened to 8 channels (zeros) so the
+        # 7x7 stem runs on the bf16x3 im2col kernel: measured 866 -> 861 img/s (2.7x the FLOPs
+        # of the zero channels; profiles/r03_stem_se_ab.txt), so the scalar exact path stays
+        self.stem_pad = int(os.environ.get("PLD_STEM_PAD", "0"))
+        if self.stem_pad:
+            self.stem.pad_input_channels(self.stem_pad)
         self.init_weights(seed)
         self._alloc()
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
@@ -201,6 +207,8 @@ class RedWebFF:
                 self.gact[name] = torch.empty(shape, device=dev)
 
         new("input", (B, H, W, 3), grad=False)
+        if self.stem_pad:
+            new("input_pad", (B, H, W, self.stem_pad), grad=False)
         h, w = H // 2, W // 2
         new("conv1_pre", (B, h, w, 64), grad=False)
         new("conv1_relu", (B, h, w, 64))
@@ -296,10 +304,11 @@ class RedWebFF:
         H, W = self.H, self.W
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
-        args = K.conv_args(A["input"], None, 7, 7, 2, 3, 3, h, w, 64,
-                           math=self._math(self.stem, h, w))
-        self.stem_bn.conv_fwd_stats(args, self.stem.w_nat, self.stem.b, A["conv1_pre"], B * h * w,
-                                    training)
+        x0, w0 = A["input"], self.stem.w_nat
+        if self.stem_pad:  # the 3-channel input widened with zeros (EffNetFF.stem_pad)
+            x0, w0 = K.channel_pad_affine(A["input"], self.stem_pad, A["input_pad"]), self.stem.w_pad
+        args = K.conv_args(x0, None, 7, 7, 2, 3, 3, h, w, 64, math=self._math(self.stem, h, w))
+        self.stem_bn.conv_fwd_stats(args, w0, self.stem.b, A["conv1_pre"], B * h * w, training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
         K.maxpool2d_fwd(A["conv1_relu"], 3, 2, 1, 1, A["pool1_pool"], self.pool_argmax)
         x = A["pool1_pool"]

@@ -307,6 +307,46 @@ def test_conv_prologue_every_schedule(cuda, case, math):
         assert rel_err(y, y_ref) < tol, (t, rel_err(y, y_ref))
 
 
+@pytest.mark.parametrize("math", MATHS)
+@pytest.mark.parametrize("k,cout,cpad,norm", [(3, 32, 8, True), (7, 64, 8, False),
+                                             (3, 32, 4, True), (7, 64, 4, False)])
+def test_padded_stem(cuda, math, k, cout, cpad, norm):
+    """The stems' widened input: pld_channel_pad_affine (normalisation + zero channels) then the
+    stride-2 conv with a zero-padded filter equals the 3-channel conv of the normalised input
+    (EfficientNetB0 3x3 TF-SAME / ResNet-50 7x7 pad 3; padding taps zero either way)."""
+    torch.manual_seed(k * cpad)
+    n, h, w = 2, 30, 26
+    x = torch.rand(n, h, w, 3, dtype=torch.float64) * 255
+    wt = torch.randn(k, k, 3, cout, dtype=torch.float64) / np.sqrt(k * k * 3)
+    sc = torch.tensor([0.017, 0.018, 0.0175], dtype=torch.float64) if norm else None
+    sh = torch.tensor([-2.1, -2.0, -1.8], dtype=torch.float64) if norm else None
+    xn = x * sc + sh if norm else x
+    if k == 3:
+        pt, pb = OE.correct_pad(h, k)
+        pl, pr = OE.correct_pad(w, k)
+    else:
+        pt = pb = pl = pr = 3
+    oh, ow = (h + pt + pb - k) // 2 + 1, (w + pl + pr - k) // 2 + 1
+    y_ref = OE.conv(xn.permute(0, 3, 1, 2), wt, None, 2, (pt, pb, pl, pr)).permute(0, 2, 3, 1)
+    gx = dev(x, cuda)
+    xp = torch.full((n, h, w, cpad), 7.0, device=cuda)  # stale contents must be overwritten
+    K.channel_pad_affine(gx, cpad, xp, dev(sc, cuda) if norm else None,
+                         dev(sh, cuda) if norm else None)
+    torch.cuda.synchronize()
+    assert torch.all(xp[..., 3:] == 0)
+    assert rel_err(xp[..., :3], xn) < 1e-6
+    wp = torch.zeros(k, k, cpad, cout, dtype=torch.float64)
+    wp[:, :, :3] = wt
+    args = K.conv_args(xp, None, k, k, 2, pt, pl, oh, ow, cout, math=math)
+    wn = K.filter_to_native(dev(wp, cuda))
+    if math == "bf16x3" and cpad % 8 == 0:
+        K.filter_split(wn)
+    y = torch.empty(n, oh, ow, cout, device=cuda)
+    K.conv2d_fwd(args, wn, None, y)
+    torch.cuda.synchronize()
+    assert rel_err(y, y_ref) < CONV_TOL[math], rel_err(y, y_ref)
+
+
 def test_bn_train_coeffs(cuda):
     """scale = gamma*invstd, shift = beta - mean*scale: act(x*scale + shift) == bn_apply."""
     torch.manual_seed(3)
