@@ -139,47 +139,51 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgParams p) {
       }
     }
   }
-  // this wave's [64 rows][NW] chunk through LDS (the input tile's space, once every wave is
-  // done reading it), then whole row segments to HBM
+  // the workgroup's [64 rows][N] output tile through LDS (the input tile's space, once every
+  // wave is done reading it), then stored as the one contiguous run of y it is: float4 stores
+  // when N % 4 == 0 (the per-wave column chunks wrote 16-40-byte pieces of 64 rows)
   __syncthreads();
-  constexpr int LO = NW + 4;
-  float* sw = sa + wave * 64 * LO;
+  const int LO = p.N + 4;
 #pragma unroll
-  for (int j = 0; j < NW; ++j) sw[lane * LO + j] = acc[j];
-  __builtin_amdgcn_wave_barrier();
-  const int ncol = min(NW, p.N - nb);
-  if (ncol <= 0) return;
-  if (!p.acc) {
-    for (int e = lane; e < rows * ncol; e += 64) {
-      const int r = e / ncol, j = e - r * ncol;
-      p.y[(m0 + r) * p.N + nb + j] = sw[r * LO + j];
+  for (int j = 0; j < NW; ++j)
+    if (nb + j < p.N) sa[lane * LO + nb + j] = acc[j];
+  __syncthreads();
+  const int N = p.N;
+  if (N % 4 == 0 && (reinterpret_cast<uintptr_t>(p.y) & 15) == 0) {
+    const int nq = N / 4, tq = rows * nq;
+    float4* dst = reinterpret_cast<float4*>(p.y + m0 * N);
+    constexpr int U = 4;  // accumulate: U destination quads fetched before their stores
+    for (int e0 = tid; e0 < tq; e0 += 256 * U) {
+      float4 old[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        old[u] = (p.acc && e < tq) ? dst[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        if (e < tq) {
+          const int r = e / nq, q = e - r * nq;
+          float4 v = *reinterpret_cast<const float4*>(sa + r * LO + 4 * q);
+          if (p.acc) v = add4(v, old[u]);
+          dst[e] = v;
+        }
+      }
     }
     return;
   }
-  // accumulate: 8 destination values fetched together per trip (one HBM latency per 8
-  // read-modify-writes: the compiler will not reorder them across the possibly aliasing stores)
-  constexpr int U = 8;
-  for (int e0 = lane; e0 < rows * ncol; e0 += 64 * U) {
-    float old[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = e0 + 64 * u;
-      const int r = e / ncol, j = e - r * ncol;
-      old[u] = e < rows * ncol ? p.y[(m0 + r) * p.N + nb + j] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = e0 + 64 * u;
-      if (e >= rows * ncol) break;
-      const int r = e / ncol, j = e - r * ncol;
-      p.y[(m0 + r) * p.N + nb + j] = old[u] + sw[r * LO + j];
-    }
+  for (int e = tid; e < rows * N; e += 256) {
+    const int r = e / N, j = e - r * N;
+    const float v = sa[r * LO + j];
+    float* d = p.y + (m0 + r) * N + j;
+    *d = p.acc ? *d + v : v;
   }
 }
 
 static int pg_launch(PgParams& p, int pro, hipStream_t st) {
   const int nw = (p.N + 3) / 4;
-  const size_t lds = sizeof(float) * std::max(64 * (p.K + 4), 4 * 64 * (12 + 4));
+  const size_t lds = sizeof(float) * 64 * (std::max(p.K, p.N) + 4);
   const unsigned grid = cdiv(p.M, 64);
   const int mq = (int)cdiv(64, 256 / (p.K / 4));  // passes of rpp rows per thread
 #define PG3(NWV, MQV)                                                                      \

@@ -6,9 +6,12 @@
 // reach ~3.5 TB/s on them. Here a 256-thread workgroup owns 64 consecutive rows (one contiguous
 // 64*K-float block of `a`, read fully coalesced and transposed through LDS so each lane holds
 // its row in VGPRs); its 4 waves split the output columns, the filter row of each column is
-// wave-uniform (scalar loads: the FMAs take it as an SGPR operand), and the outputs go back
-// through LDS in CH-column chunks so every store instruction writes whole 32/64-byte row
-// segments. Exact fp32 fmaf chains in k order.
+// wave-uniform (scalar loads: the FMAs take it as an SGPR operand), and the workgroup's whole
+// [64][N] output tile goes back through LDS, to be stored as the one contiguous run of `out` it
+// is (round 3: the per-wave column chunks wrote 32-64-byte pieces of 64 rows per instruction,
+// 3.1-3.6 TB/s on the 16->96 and 24->144 expand convs). Exact fp32 fmaf chains in k order.
+#include <algorithm>
+
 #include "common.h"
 #include "conv_common.h"
 
@@ -23,9 +26,11 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
                                                       float* __restrict__ out, int M, int N,
                                                       int acc, double* __restrict__ stats) {
   constexpr int LA = KR + THIN_PAD;  // LDS row stride of the staged a tile
-  constexpr int LO = CH + THIN_PAD;  // LDS row stride of a wave's output chunk
-  __shared__ __attribute__((aligned(16))) float sa[64 * LA];
-  __shared__ __attribute__((aligned(16))) float so[4][64 * LO];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sa = smem;                  // [64][LA]
+  float* so = smem;                  // [64][N + THIN_PAD]: the whole output tile (over sa, once
+                                     // every wave holds its row in registers)
+  const int LO = N + THIN_PAD;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar filter loads
   const long m0 = (long)blockIdx.x * 64;
@@ -51,9 +56,8 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
     const float4 v = *reinterpret_cast<const float4*>(sa + lane * LA + k);
     x[k] = v.x; x[k + 1] = v.y; x[k + 2] = v.z; x[k + 3] = v.w;
   }
-  // the 4 waves share the 64 rows and take CH-column chunks round-robin; from here on each wave
-  // only touches its own staging buffer (in-order LDS within a wave: no workgroup barrier)
-  float* sw = so[wave];
+  __syncthreads();  // sa is dead: the output tile reuses its space (one more block per CU)
+  // the 4 waves share the 64 rows and take CH-column chunks round-robin into the LDS tile
   for (int n0 = wave * CH; n0 < N; n0 += 4 * CH) {
     float o[CH];
 #pragma unroll
@@ -66,53 +70,47 @@ __global__ __launch_bounds__(256) void thin1x1_kernel(const float* __restrict__ 
     }
 #pragma unroll
     for (int j = 0; j < CH; j += 4)
-      *reinterpret_cast<float4*>(sw + lane * LO + j) = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
-    __builtin_amdgcn_wave_barrier();
-    if (stats) {
-      // BN batch statistics of the output (the BatchNormalization that follows the conv):
-      // per column, sum and sum of squares over this workgroup's rows in fp64 — lane (j, part)
-      // sums rows part, part + 64/CH, ... of column j, then a fixed butterfly over the parts.
-      // Partials [N][gridDim.x][2] (bn.hip's finalize layout).
-      constexpr int NP = 64 / CH;
-      const int j = lane % CH, part = lane / CH;
+      *reinterpret_cast<float4*>(so + lane * LO + n0 + j) =
+          make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+  }
+  __syncthreads();
+  if (stats) {
+    // BN batch statistics of the output (the BatchNormalization that follows the conv): per
+    // column, sum and sum of squares over this workgroup's rows in fp64 (thread = column; rows
+    // in order). Partials [N][gridDim.x][2] (bn.hip's finalize layout).
+    for (int j = tid; j < N; j += 256) {
       double s1 = 0.0, s2 = 0.0;
-      for (int r = part; r < rows; r += NP) {
-        const double v = (double)sw[r * LO + j];
+      for (int r = 0; r < rows; ++r) {
+        const double v = (double)so[r * LO + j];
         s1 += v;
         s2 += v * v;
       }
-#pragma unroll
-      for (int o = CH; o < 64; o <<= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-      }
-      if (lane < CH)
-        *reinterpret_cast<double2*>(stats + ((long)(n0 + j) * gridDim.x + blockIdx.x) * 2) =
-            make_double2(s1, s2);
+      *reinterpret_cast<double2*>(stats + ((long)j * gridDim.x + blockIdx.x) * 2) =
+          make_double2(s1, s2);
     }
-    // rows x CH chunk: CH/4 lanes per row, 64 / (CH/4) rows per store instruction
-    constexpr int QPR = CH / 4;
-    float4 old[QPR];  // accumulate: the destination quads fetched before any store
+  }
+  // the tile's rows are one contiguous [rows][N] run of out: fully coalesced float4 stores
+  // (chunked per wave, each instruction wrote 32-64-byte pieces of 64 different rows)
+  const int nq = N / 4, tq = rows * nq;
+  constexpr int U = 4;  // accumulate: U destination quads fetched before their stores
+  float4* dst = reinterpret_cast<float4*>(out + m0 * N);
+  for (int e0 = tid; e0 < tq; e0 += 256 * U) {
+    float4 old[U];
 #pragma unroll
-    for (int j = 0; j < QPR; ++j) {
-      const int e = lane + 64 * j;
-      const int r = e / QPR, q = e % QPR;
-      old[j] = (acc && r < rows)
-                   ? *reinterpret_cast<const float4*>(out + (m0 + r) * N + n0 + 4 * q)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 256 * u;
+      old[u] = (acc && e < tq) ? dst[e] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int j = 0; j < QPR; ++j) {
-      const int e = lane + 64 * j;
-      const int r = e / QPR, q = e % QPR;
-      if (r < rows) {
-        float4 v = *reinterpret_cast<const float4*>(sw + r * LO + 4 * q);
-        float4* d = reinterpret_cast<float4*>(out + (m0 + r) * N + n0 + 4 * q);
-        if (acc) v = add4(v, old[j]);
-        *d = v;
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 256 * u;
+      if (e < tq) {
+        const int r = e / nq, q = e - r * nq;
+        float4 v = *reinterpret_cast<const float4*>(so + r * LO + 4 * q);
+        if (acc) v = add4(v, old[u]);
+        dst[e] = v;
       }
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -120,11 +118,12 @@ template <int KR>
 static void thin_launch(const float* a, const float* b, const float* bias, float* out, int M,
                         int N, int acc, double* stats, hipStream_t st) {
   const unsigned grid = (unsigned)cdiv(M, 64);
+  const size_t lds = sizeof(float) * 64 * (std::max(KR, N) + THIN_PAD);
   // CH = 16 only when the chunks split evenly over the 4 waves (N = 144: 18 chunks of 8 balance
   // 5/5/4/4, 9 chunks of 16 would leave three waves idle a third of the time)
   if (N % 64 == 0 && N >= 128)
-    thin1x1_kernel<KR, 16><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc, stats);
-  else thin1x1_kernel<KR, 8><<<grid, 256, 0, st>>>(a, b, bias, out, M, N, acc, stats);
+    thin1x1_kernel<KR, 16><<<grid, 256, lds, st>>>(a, b, bias, out, M, N, acc, stats);
+  else thin1x1_kernel<KR, 8><<<grid, 256, lds, st>>>(a, b, bias, out, M, N, acc, stats);
 }
 
 static bool thin_kr_ok(int kr) { return kr % 8 == 0 && kr >= 8 && kr <= 48; }
