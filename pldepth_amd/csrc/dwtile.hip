@@ -3,8 +3,9 @@
 // the block's expand BN + swish applied to the input as it is staged and, optionally, the batch
 // statistics of the output (the BN that follows) gathered in the epilogue.
 //
-// A workgroup owns a TO-wide output tile of 4 CQ = 32 channels (the last group masked when
-// C % 32 == 16). The
+// A workgroup walks a contiguous run of TO-wide output tiles of one group of 4 CQ = 32 channels
+// (the last group masked when C % 32 == 16), the next tile's window loads issued before the
+// current tile's FMAs so that they overlap (tile_plan sizes the grid to one resident round). The
 // ((TO - 1) S + K)^2 input window of those channels is read once (coalesced: CQ * 16 contiguous
 // bytes per pixel), activated once per element (the register-window kernel in dwse.hip
 // re-activated every overlapping window load: ~4x the exp / rcp work at k5) and stored in LDS,
@@ -13,7 +14,7 @@
 // and R rows: it walks the (R - 1) S + K input rows of its column window once, feeding every tap
 // of every output row it reaches from registers (filter taps preloaded), in the same (ty, tx)
 // summation order as the direct loop. Statistics: per-thread fp64 sums of its outputs, combined
-// over the workgroup in a fixed order into [C][tiles][2] partials (bn.hip's finalize layout).
+// over the workgroup in a fixed order into [C][workgroups][2] partials (bn.hip's finalize layout).
 #include <algorithm>
 
 #include "common.h"
@@ -32,6 +33,7 @@ struct Geo {
   double* stats;        // [C][gridDim.x][2] or NULL
   int n, h, wd, c, oh, ow, pt, pl;
   int tiles_x, tiles_y;
+  int per;              // tiles per workgroup (a contiguous run of its channel group's tiles)
 };
 
 __device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
@@ -42,12 +44,33 @@ __device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
   return acc;
 }
 
-// output rows per tile: 4 per thread (the k5 filter, 25 float4 taps, stays in registers)
+// output rows per tile: 4 per thread (k5 stride 1) / 2 (stride 2)
 __host__ __device__ constexpr int tile_rows(int s, int cq) { return (256 / (cq * (s == 1 ? 16 : 8))) * (s == 1 ? 4 : 2); }
 
+// Workgroups per launch: every workgroup of the grid resident at once (DW_MINB per CU: the
+// launch bound holds every instantiation's VGPRs to that, the windows fit the LDS), each walking a contiguous run of
+// tiles of its channel group with the next tile's window loads in flight while the current one
+// is computed (one tile per workgroup left the load, the prologue and the FMA/LDS phases
+// serialised: 2-3.9 TB/s at 14^2-56^2).
+#ifndef PLD_DW_MINB
+#define PLD_DW_MINB 2
+#endif
+constexpr int RESIDENT = PLD_DW_MINB * 256;
+
+__host__ __device__ constexpr int tile_cols(int s) { return s == 1 ? 16 : 8; }
+
+// tiles per workgroup and workgroups per channel group (grid.x = the statistics' part count)
+static void tile_plan(int n, int oh, int ow, int s, int c, int& per, int& nbx) {
+  const long nsp = (long)n * cdiv(oh, tile_rows(s, 8)) * cdiv(ow, tile_cols(s));
+  const long ncg = cdiv(c, 32);
+  const long slots = std::max<long>(1, RESIDENT / ncg);
+  per = (int)cdiv(nsp, slots);
+  nbx = (int)cdiv(nsp, per);
+}
+
 template <int K, int S, int CQ, int ACT>  // ACT < 0: no prologue
-__global__ __launch_bounds__(256) void dw_fwd_tile_kernel(Geo g) {
-  constexpr int TO = S == 1 ? 16 : 8;             // output tile width
+__global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
+  constexpr int TO = tile_cols(S);                // output tile width
   constexpr int TOH = tile_rows(S, CQ);           // output tile height
   constexpr int TI = (TO - 1) * S + K;            // input window width
   constexpr int TIR = (TOH - 1) * S + K;          // input window height
@@ -58,123 +81,151 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(Geo g) {
   constexpr int NR = (R - 1) * S + K;             // input rows a thread walks
   constexpr int NE = TIR * TI * CQ;               // window float4s
   constexpr int NL = (NE + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) float4 tile[];  // [TI][COLS][CQ]
+  static_assert(256 % CQ == 0, "a thread's staged channel quad is tid % CQ on every load");
+  extern __shared__ __attribute__((aligned(16))) float4 tile[];  // [TIR][COLS][CQ], [K K][CQ]
+  float4* ftile = tile + TIR * COLS * CQ;
   const int tid = threadIdx.x;
-  const int sp = blockIdx.x;
-  const int img = sp / (g.tiles_x * g.tiles_y);
-  const int rr = sp - img * g.tiles_x * g.tiles_y;
-  const int oy0 = (rr / g.tiles_x) * TOH, ox0 = (rr % g.tiles_x) * TO;
   const int cb = blockIdx.y * CQ * 4;             // first channel of the group
-  const int iy0 = oy0 * S - g.pt, ix0 = ox0 * S - g.pl;
-  const float* xb = g.x + (long)img * g.h * g.wd * g.c + cb;
-
-  // ---- stage the window: loads first, then the prologue and the LDS stores ----
-  float4 v[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int e = tid + 256 * i;
-    const int q = e % CQ, px = e / CQ;
-    const int wy = px / TI, wx = px - wy * TI;
-    const int iy = iy0 + wy, ix = ix0 + wx;
-    const bool ok = e < NE && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd &&
-                    cb + 4 * q < g.c;
-    v[i] = ok ? *reinterpret_cast<const float4*>(xb + ((long)iy * g.wd + ix) * g.c + 4 * q)
-              : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int e = tid + 256 * i;
-    if (e >= NE) break;
-    const int q = e % CQ, px = e / CQ;
-    const int wy = px / TI, wx = px - wy * TI;
-    const int iy = iy0 + wy, ix = ix0 + wx;
-    float4 a = v[i];
-    if (ACT >= 0 && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd &&
-        cb + 4 * q < g.c) {
-      // bn_apply's arithmetic, then the activation (TF pads the activated map with zeros)
-      const int c0 = cb + 4 * q;
-      const float4 mu = *reinterpret_cast<const float4*>(g.mean + c0);
-      const float4 is = *reinterpret_cast<const float4*>(g.invstd + c0);
-      const float4 ga = *reinterpret_cast<const float4*>(g.gamma + c0);
-      const float4 be = *reinterpret_cast<const float4*>(g.beta + c0);
-      a = make_float4(act_fwd(ACT, ((a.x - mu.x) * is.x) * ga.x + be.x),
-                      act_fwd(ACT, ((a.y - mu.y) * is.y) * ga.y + be.y),
-                      act_fwd(ACT, ((a.z - mu.z) * is.z) * ga.z + be.z),
-                      act_fwd(ACT, ((a.w - mu.w) * is.w) * ga.w + be.w));
-    }
-    const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
-    tile[(wy * COLS + col) * CQ + q] = a;
-  }
-  const int q = tid % CQ, oc = (tid / CQ) % TO, rg = tid / (CQ * TO);
+  const int ntx = g.tiles_x, nt = g.tiles_x * g.tiles_y;
+  const int nsp = g.n * nt;
+  const int sp0 = blockIdx.x * g.per, sp1 = min(nsp, sp0 + g.per);
+  const int q = tid % CQ;                         // staged quad (all loads) = computed quad
   const bool qok = cb + 4 * q < g.c;  // the last group of a C % 32 == 16 layer is half full
   const float* fq = g.w + (qok ? cb + 4 * q : 0);  // this thread's filter quad: tap t at fq + t C
-  float4 acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto lds_row = [&](int wy, float4 (&row)[K]) {
-#pragma unroll
-    for (int tx = 0; tx < K; ++tx) {
-      const int wx = oc * S + tx;
-      const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
-      row[tx] = tile[(wy * COLS + col) * CQ + q];
-    }
-  };
+  float4 mu, is, ga, be;
+  if (ACT >= 0 && qok) {
+    mu = *reinterpret_cast<const float4*>(g.mean + cb + 4 * q);
+    is = *reinterpret_cast<const float4*>(g.invstd + cb + 4 * q);
+    ga = *reinterpret_cast<const float4*>(g.gamma + cb + 4 * q);
+    be = *reinterpret_cast<const float4*>(g.beta + cb + 4 * q);
+  }
+  // k3: the 9 taps in registers; k5: the 25 taps staged once in LDS (filter loads inside the
+  // tile loop would queue behind the prefetched window and wait for it)
+  float4 f3[K == 3 ? 3 : 1][K == 3 ? 3 : 1];
   if constexpr (K == 3) {
-    // the 9 taps in registers; each of the (R - 1) S + K input rows of the column window read
-    // once and fed to every output row it reaches
-    float4 f[K][K];
 #pragma unroll
     for (int ty = 0; ty < K; ++ty)
 #pragma unroll
-      for (int tx = 0; tx < K; ++tx) f[ty][tx] = *reinterpret_cast<const float4*>(fq + (ty * K + tx) * g.c);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      float4 row[K];
-      lds_row(rg * R * S + j, row);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int ty = j - r * S;  // compile-time after unrolling
-        if (ty < 0 || ty >= K) continue;
-#pragma unroll
-        for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[ty][tx]);
-      }
-    }
+      for (int tx = 0; tx < K; ++tx) f3[ty][tx] = *reinterpret_cast<const float4*>(fq + (ty * K + tx) * g.c);
   } else {
-    // k5: one filter row (5 taps) in registers at a time, ty outer; each output row re-reads
-    // its input row per ty (25 taps in registers plus the unrolled window do not fit)
-    __syncthreads();
-#pragma unroll 1
-    for (int ty = 0; ty < K; ++ty) {
-      float4 f[K];
-#pragma unroll
-      for (int tx = 0; tx < K; ++tx) f[tx] = *reinterpret_cast<const float4*>(fq + (ty * K + tx) * g.c);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float4 row[K];
-        lds_row(rg * R * S + r * S + ty, row);
-#pragma unroll
-        for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[tx]);
-      }
+    for (int e = tid; e < K * K * CQ; e += 256) {
+      const int t = e / CQ, qq = e % CQ;
+      ftile[e] = cb + 4 * qq < g.c ? *reinterpret_cast<const float4*>(g.w + t * g.c + cb + 4 * qq)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // ---- store (+ statistics) ----
-  const int ox = ox0 + oc;
+  auto origin = [&](int sp, int& img, int& oy0, int& ox0) {
+    img = sp / nt;
+    const int rr = sp - img * nt;
+    oy0 = (rr / ntx) * TOH;
+    ox0 = (rr % ntx) * TO;
+  };
+  float4 v[NL];
+  auto load_window = [&](int sp) {
+    int img, oy0, ox0;
+    origin(sp, img, oy0, ox0);
+    const int iy0 = oy0 * S - g.pt, ix0 = ox0 * S - g.pl;
+    const float* xb = g.x + (long)img * g.h * g.wd * g.c + cb;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = tid + 256 * i;
+      const int px = e / CQ;
+      const int wy = px / TI, wx = px - wy * TI;
+      const int iy = iy0 + wy, ix = ix0 + wx;
+      const bool ok = e < NE && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd && qok;
+      v[i] = ok ? *reinterpret_cast<const float4*>(xb + ((long)iy * g.wd + ix) * g.c + 4 * q)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  const int oc = (tid / CQ) % TO, rg = tid / (CQ * TO);
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (ox < g.ow && qok) {
+  if (sp0 < sp1) load_window(sp0);
+  for (int sp = sp0; sp < sp1; ++sp) {
+    int img, oy0, ox0;
+    origin(sp, img, oy0, ox0);
+    const int iy0 = oy0 * S - g.pt, ix0 = ox0 * S - g.pl;
+    __syncthreads();  // the previous tile's window is no longer read
+    // ---- the prologue and the LDS stores of this tile's window ----
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int oy = oy0 + rg * R + r;
-      if (oy >= g.oh) break;
-      *reinterpret_cast<float4*>(g.y + (((long)img * g.oh + oy) * g.ow + ox) * g.c + cb + 4 * q) =
-          acc[r];
-      if (g.stats) {
-        const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+    for (int i = 0; i < NL; ++i) {
+      const int e = tid + 256 * i;
+      if (e >= NE) break;
+      const int px = e / CQ;
+      const int wy = px / TI, wx = px - wy * TI;
+      const int iy = iy0 + wy, ix = ix0 + wx;
+      float4 a = v[i];
+      if (ACT >= 0 && (unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.wd && qok) {
+        // bn_apply's arithmetic, then the activation (TF pads the activated map with zeros)
+        a = make_float4(act_fwd(ACT, ((a.x - mu.x) * is.x) * ga.x + be.x),
+                        act_fwd(ACT, ((a.y - mu.y) * is.y) * ga.y + be.y),
+                        act_fwd(ACT, ((a.z - mu.z) * is.z) * ga.z + be.z),
+                        act_fwd(ACT, ((a.w - mu.w) * is.w) * ga.w + be.w));
+      }
+      const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
+      tile[(wy * COLS + col) * CQ + q] = a;
+    }
+    __syncthreads();
+    if (sp + 1 < sp1) load_window(sp + 1);  // in flight under this tile's FMAs
+    float4 acc[R];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const double d = a4[u];
-          s1[u] += d;
-          s2[u] += d * d;
+    for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto lds_row = [&](int wy, float4 (&row)[K]) {
+#pragma unroll
+      for (int tx = 0; tx < K; ++tx) {
+        const int wx = oc * S + tx;
+        const int col = S == 1 ? wx : (wx & 1) * TIH + (wx >> 1);
+        row[tx] = tile[(wy * COLS + col) * CQ + q];
+      }
+    };
+    if constexpr (K == 3) {
+      // each of the (R - 1) S + K input rows of the column window read once and fed to every
+      // output row it reaches
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        float4 row[K];
+        lds_row(rg * R * S + j, row);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int ty = j - r * S;  // compile-time after unrolling
+          if (ty < 0 || ty >= K) continue;
+#pragma unroll
+          for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f3[ty][tx]);
+        }
+      }
+    } else {
+      // k5: one filter row (5 taps) at a time, ty outer; each output row re-reads its input row
+      // per ty (25 taps in registers plus the unrolled window do not fit)
+#pragma unroll 1
+      for (int ty = 0; ty < K; ++ty) {
+        float4 f[K];
+#pragma unroll
+        for (int tx = 0; tx < K; ++tx) f[tx] = ftile[(ty * K + tx) * CQ + q];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          float4 row[K];
+          lds_row(rg * R * S + r * S + ty, row);
+#pragma unroll
+          for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[tx]);
+        }
+      }
+    }
+    // ---- store (+ statistics) ----
+    const int ox = ox0 + oc;
+    if (ox < g.ow && qok) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int oy = oy0 + rg * R + r;
+        if (oy >= g.oh) break;
+        *reinterpret_cast<float4*>(g.y + (((long)img * g.oh + oy) * g.ow + ox) * g.c + cb + 4 * q) =
+            acc[r];
+        if (g.stats) {
+          const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double d = a4[u];
+            s1[u] += d;
+            s2[u] += d * d;
+          }
         }
       }
     }
@@ -197,27 +248,28 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(Geo g) {
       for (int u = 0; u < 8; ++u) t[u] += red[(tid + CQ * j) * 8 + u];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      *reinterpret_cast<double2*>(g.stats + ((long)(cb + 4 * tid + u) * gridDim.x + sp) * 2) =
+      *reinterpret_cast<double2*>(g.stats + ((long)(cb + 4 * tid + u) * gridDim.x + blockIdx.x) * 2) =
           make_double2(t[u], t[4 + u]);
   }
 }
 
 template <int K, int S, int CQ>
 static size_t lds_bytes() {
-  constexpr int TO = S == 1 ? 16 : 8;
+  constexpr int TO = tile_cols(S);
   constexpr int TI = (TO - 1) * S + K;
   constexpr int TIR = (tile_rows(S, CQ) - 1) * S + K;
   constexpr int COLS = S == 1 ? TI : 2 * ((TI + 1) / 2);
-  const size_t win = sizeof(float4) * TIR * COLS * CQ;
+  const size_t win = sizeof(float4) * (TIR * COLS * CQ + (K == 5 ? K * K * CQ : 0));
   return std::max(win, sizeof(double) * 256 * 8);
 }
 
 template <int K, int S, int CQ>
 static void launch(Geo& g, int act, hipStream_t st) {
-  constexpr int TO = S == 1 ? 16 : 8;
-  g.tiles_x = (int)cdiv(g.ow, TO);
+  g.tiles_x = (int)cdiv(g.ow, tile_cols(S));
   g.tiles_y = (int)cdiv(g.oh, tile_rows(S, CQ));
-  dim3 grid(g.tiles_x * g.tiles_y * g.n, (int)cdiv(g.c, 4 * CQ));
+  int nbx;
+  tile_plan(g.n, g.oh, g.ow, S, g.c, g.per, nbx);
+  dim3 grid(nbx, (int)cdiv(g.c, 4 * CQ));
   const size_t lds = lds_bytes<K, S, CQ>();
   if (!g.mean) dw_fwd_tile_kernel<K, S, CQ, -1><<<grid, 256, lds, st>>>(g);
   else if (act == ACT_SWISH) dw_fwd_tile_kernel<K, S, CQ, ACT_SWISH><<<grid, 256, lds, st>>>(g);
@@ -237,8 +289,9 @@ extern "C" int pld__dw_tiled_ok(int k, int s, int c) {
 }
 
 extern "C" int pld__dw_tiled_parts(int n, int oh, int ow, int s, int c) {
-  const int to = s == 1 ? 16 : 8, toh = dwt::tile_rows(s, 8);
-  return (int)(cdiv(oh, toh) * cdiv(ow, to) * n);
+  int per, nbx;
+  dwt::tile_plan(n, oh, ow, s, c, per, nbx);
+  return nbx;
 }
 
 extern "C" int pld__dw_fwd_tiled(const float* x, int n, int h, int w, int c, const float* wdw,

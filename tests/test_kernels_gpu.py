@@ -523,7 +523,10 @@ def test_residual_inplace_vector_and_scalar_paths(cuda, shape):
                                          # the LDS-tiled kernel (c % 16 == 0): 4- and 8-quad
                                          # channel groups, ragged tiles, both strides
                                          (2, 37, 21, 48, 5, 1), (1, 35, 19, 64, 3, 2),
-                                         (2, 18, 33, 32, 3, 1), (1, 17, 23, 96, 5, 2)])
+                                         (2, 18, 33, 32, 3, 1), (1, 17, 23, 96, 5, 2),
+                                         # grids smaller than the tile count: each workgroup
+                                         # walks a run of tiles (window prefetch)
+                                         (8, 112, 112, 32, 5, 1), (8, 112, 112, 64, 3, 2)])
 def test_dwconv(cuda, n, h, w, c, k, s):
     torch.manual_seed(k * 10 + s)
     x = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)
@@ -1223,7 +1226,10 @@ def test_wide1x1(cuda, n, h, w, cin, cout):
 
 @pytest.mark.parametrize("n,h,w,c,k,s,pro", [(2, 37, 21, 48, 5, 1, True), (1, 35, 19, 64, 3, 2, True),
                                              (2, 18, 33, 32, 3, 1, False),
-                                             (1, 9, 13, 12, 5, 1, True)])
+                                             (1, 9, 13, 12, 5, 1, True),
+                                             (8, 112, 112, 32, 3, 1, True),
+                                             (4, 56, 56, 1152, 5, 1, True),
+                                             (4, 57, 55, 240, 5, 2, False)])
 def test_dwconv_fwd_bn_stats(cuda, n, h, w, c, k, s, pro):
     """pld_dwconv_fwd_bn_stats (the output's BN statistics from the tiled kernel's epilogue; the
     c % 16 != 0 case through the register kernel + pld_bn_stats) == pld_dwconv_fwd_bn +
