@@ -29,10 +29,12 @@ struct DwGeom {
 };
 
 __device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
-  acc.x += v.x * f.x;
-  acc.y += v.y * f.y;
-  acc.z += v.z * f.z;
-  acc.w += v.w * f.w;
+  // explicit fused multiply-adds: every tap rounds once whatever the compiler makes of the
+  // conditional rows around it (the tiled and register-window dgrads agree bit for bit)
+  acc.x = fmaf(v.x, f.x, acc.x);
+  acc.y = fmaf(v.y, f.y, acc.y);
+  acc.z = fmaf(v.z, f.z, acc.z);
+  acc.w = fmaf(v.w, f.w, acc.w);
   return acc;
 }
 
@@ -718,6 +720,9 @@ static DwGeom dw_geom(int n, int h, int w, int c, int s, int pt, int pl, int oh,
 // dwtile.hip: the LDS-tiled forward (C % 16 == 0), optionally gathering the output's BN partials
 extern "C" int pld__dw_tiled_ok(int k, int s, int c);
 extern "C" int pld__dw_tiled_parts(int n, int oh, int ow, int s, int c);
+extern "C" int pld__dw_dgrad_tiled(const float* dy, int n, int h, int w, int c, const float* wdw,
+                                   int k, int pad_t, int pad_l, int oh, int ow, float* dx,
+                                   int accumulate, hipStream_t st);
 extern "C" int pld__dw_fwd_tiled(const float* x, int n, int h, int w, int c, const float* wdw,
                                  int k, int s, int pad_t, int pad_l, int oh, int ow,
                                  const float* mean, const float* invstd, const float* gamma,
@@ -842,6 +847,13 @@ static int dw_dgrad_impl(const float* dy, int n, int h, int w, int c, const floa
   hipStream_t st = as_stream(stream);
   const DwBnb bb = bnb ? *bnb : DwBnb{};
   const bool B = bnb != nullptr;
+  if (s == 1 && !bnb && pld__dw_tiled_ok(k, 1, c) && pad_t < k && pad_l < k && aligned16(dy) &&
+      aligned16(dx) && aligned16(wdw)) {
+    // LDS-tiled (each dy element read once per workgroup instead of once per overlapping
+    // register window: 2-3.5x the dy bytes from HBM at 14^2-28^2); same sums bit for bit
+    if (grid_out) *grid_out = 0;
+    return pld__dw_dgrad_tiled(dy, n, h, w, c, wdw, k, pad_t, pad_l, oh, ow, dx, accumulate, st);
+  }
   if (s == 1) {
     constexpr int T = 4, R = 4;
     const int rgroups = (h + R - 1) / R;

@@ -34,13 +34,16 @@ struct Geo {
   int n, h, wd, c, oh, ow, pt, pl;
   int tiles_x, tiles_y;
   int per;              // tiles per workgroup (a contiguous run of its channel group's tiles)
+  int accum;            // DG: y += result
 };
 
 __device__ __forceinline__ float4 fma4(float4 acc, float4 v, float4 f) {
-  acc.x += v.x * f.x;
-  acc.y += v.y * f.y;
-  acc.z += v.z * f.z;
-  acc.w += v.w * f.w;
+  // explicit fused multiply-adds: every tap rounds once whatever the compiler makes of the
+  // conditional rows around it (the tiled and register-window dgrads agree bit for bit)
+  acc.x = fmaf(v.x, f.x, acc.x);
+  acc.y = fmaf(v.y, f.y, acc.y);
+  acc.z = fmaf(v.z, f.z, acc.z);
+  acc.w = fmaf(v.w, f.w, acc.w);
   return acc;
 }
 
@@ -68,7 +71,11 @@ static void tile_plan(int n, int oh, int ow, int s, int c, int& per, int& nbx) {
   nbx = (int)cdiv(nsp, per);
 }
 
-template <int K, int S, int CQ, int ACT>  // ACT < 0: no prologue
+// DG (stride 1): the input gradient of a stride-1 depthwise conv as this correlation of dy with
+// the flipped filter, window pads K - 1 - pad; the taps of every output summed in ascending
+// (ty, tx) order of the unflipped filter, as dwconv_dgrad_s1_kernel (dwse.hip) sums them, so the
+// two paths agree bit for bit (the BN-fused dgrad epilogue stays on that kernel).
+template <int K, int S, int CQ, int ACT, bool DG = false>  // ACT < 0: no prologue
 __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
   constexpr int TO = tile_cols(S);                // output tile width
   constexpr int TOH = tile_rows(S, CQ);           // output tile height
@@ -82,6 +89,7 @@ __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
   constexpr int NE = TIR * TI * CQ;               // window float4s
   constexpr int NL = (NE + 255) / 256;
   static_assert(256 % CQ == 0, "a thread's staged channel quad is tid % CQ on every load");
+  static_assert(!DG || (S == 1 && ACT < 0), "the dgrad form is stride 1 without a prologue");
   extern __shared__ __attribute__((aligned(16))) float4 tile[];  // [TIR][COLS][CQ], [K K][CQ]
   float4* ftile = tile + TIR * COLS * CQ;
   const int tid = threadIdx.x;
@@ -179,9 +187,10 @@ __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
     };
     if constexpr (K == 3) {
       // each of the (R - 1) S + K input rows of the column window read once and fed to every
-      // output row it reaches
+      // output row it reaches (DG: rows bottom-up, window offsets K - 1 - tap)
 #pragma unroll
-      for (int j = 0; j < NR; ++j) {
+      for (int jj = 0; jj < NR; ++jj) {
+        const int j = DG ? NR - 1 - jj : jj;
         float4 row[K];
         lds_row(rg * R * S + j, row);
 #pragma unroll
@@ -189,7 +198,10 @@ __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
           const int ty = j - r * S;  // compile-time after unrolling
           if (ty < 0 || ty >= K) continue;
 #pragma unroll
-          for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f3[ty][tx]);
+          for (int tx = 0; tx < K; ++tx) {
+            if constexpr (DG) acc[r] = fma4(acc[r], row[K - 1 - tx], f3[K - 1 - ty][tx]);
+            else acc[r] = fma4(acc[r], row[tx], f3[ty][tx]);
+          }
         }
       }
     } else {
@@ -203,9 +215,9 @@ __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           float4 row[K];
-          lds_row(rg * R * S + r * S + ty, row);
+          lds_row(rg * R * S + r * S + (DG ? K - 1 - ty : ty), row);
 #pragma unroll
-          for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[tx], f[tx]);
+          for (int tx = 0; tx < K; ++tx) acc[r] = fma4(acc[r], row[DG ? K - 1 - tx : tx], f[tx]);
         }
       }
     }
@@ -216,8 +228,12 @@ __global__ __launch_bounds__(256, PLD_DW_MINB) void dw_fwd_tile_kernel(Geo g) {
       for (int r = 0; r < R; ++r) {
         const int oy = oy0 + rg * R + r;
         if (oy >= g.oh) break;
-        *reinterpret_cast<float4*>(g.y + (((long)img * g.oh + oy) * g.ow + ox) * g.c + cb + 4 * q) =
-            acc[r];
+        float4* yp = reinterpret_cast<float4*>(g.y + (((long)img * g.oh + oy) * g.ow + ox) * g.c + cb + 4 * q);
+        if (DG && g.accum) {
+          const float4 old = *yp;
+          acc[r].x += old.x; acc[r].y += old.y; acc[r].z += old.z; acc[r].w += old.w;
+        }
+        *yp = acc[r];
         if (g.stats) {
           const float a4[4] = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
 #pragma unroll
@@ -313,4 +329,25 @@ extern "C" int pld__dw_fwd_tiled(const float* x, int n, int h, int w, int c, con
   else { DWT(5, 2) }
 #undef DWT
   return check_launch("dw_fwd_tile_kernel");
+}
+
+// stride-1 input gradient through the tiled kernel (DG): dx [n][h][w][c] from dy [n][oh][ow][c]
+extern "C" int pld__dw_dgrad_tiled(const float* dy, int n, int h, int w, int c, const float* wdw,
+                                   int k, int pad_t, int pad_l, int oh, int ow, float* dx,
+                                   int accumulate, hipStream_t st) {
+  dwt::Geo g{};
+  g.x = dy; g.w = wdw; g.y = dx;
+  g.n = n; g.h = oh; g.wd = ow; g.c = c; g.oh = h; g.ow = w;
+  g.pt = k - 1 - pad_t; g.pl = k - 1 - pad_l;
+  g.accum = accumulate;
+  g.tiles_x = (int)cdiv(w, dwt::tile_cols(1));
+  g.tiles_y = (int)cdiv(h, dwt::tile_rows(1, 8));
+  int nbx;
+  dwt::tile_plan(n, h, w, 1, c, g.per, nbx);
+  dim3 grid(nbx, (int)cdiv(c, 32));
+  if (k == 3)
+    dwt::dw_fwd_tile_kernel<3, 1, 8, -1, true><<<grid, 256, dwt::lds_bytes<3, 1, 8>(), st>>>(g);
+  else
+    dwt::dw_fwd_tile_kernel<5, 1, 8, -1, true><<<grid, 256, dwt::lds_bytes<5, 1, 8>(), st>>>(g);
+  return check_launch("dw_fwd_tile_kernel(dgrad)");
 }

@@ -1090,6 +1090,10 @@ def test_conv_fwd_bn_stats(cuda, n, h, w, cin, cout):
 @pytest.mark.parametrize("n,h,w,c,k,s,pt,pl", [(2, 13, 11, 96, 3, 1, 1, 1),
                                                 (1, 9, 10, 40, 5, 1, 2, 2),
                                                 (2, 14, 12, 1152, 3, 1, 1, 1),
+                                                # the LDS-tiled stride-1 dgrad (c % 16 == 0)
+                                                # must match the fused kernel's sums bit for bit
+                                                (1, 9, 10, 48, 5, 1, 2, 2),
+                                                (4, 28, 28, 672, 5, 1, 2, 2),
                                                 (2, 15, 13, 144, 3, 2, 1, 1),
                                                 (1, 12, 14, 240, 5, 2, 1, 2)])
 def test_dwconv_dgrad_bn_bwd(cuda, n, h, w, c, k, s, pt, pl):
