@@ -1728,6 +1728,10 @@ static const Cfg kCfg[] = {
     // short-M / long-K launches (the encoder's 14x14 and 28x28 1x1 convs at batch 32: 147-294
     // tiles of 128 x 64 leave most of the 256 CUs idle): 4x the workgroups, 4 resident per CU
     {64, 64, 1, 1, 4},
+    // short-M launches with narrow-but-not-tiny N (N = 112..320 at M = 6272 / 25088): one
+    // workgroup covers 2-3x the columns of a 64 x 64 tile, so the A strip is staged once per
+    // 128 / 192 columns instead of once per 64
+    {64, 128, 1, 2, 3},  {64, 192, 1, 3, 2},
 };
 constexpr int kNumCfg = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
 
@@ -1764,7 +1768,9 @@ static void launch(GemmConvParams& p, int splits, int cfg, hipStream_t st) {
     case 7: launch_cfg<MODE, 256, 64, 4, 1>(p, splits, st); break;
     case 8: launch_cfg<MODE, 256, 128, 2, 2>(p, splits, st); break;
     case 9: launch_cfg<MODE, 128, 256, 2, 2>(p, splits, st); break;
-    default: launch_cfg<MODE, 64, 64, 2, 2>(p, splits, st); break;
+    case 10: launch_cfg<MODE, 64, 64, 2, 2>(p, splits, st); break;
+    case 11: launch_cfg<MODE, 64, 128, 2, 2>(p, splits, st); break;
+    default: launch_cfg<MODE, 64, 192, 2, 2>(p, splits, st); break;
   }
 }
 
