@@ -3,6 +3,7 @@
 PyTorch is plumbing here: tensors provide device memory and the current HIP stream; every
 computation is a call into libpldepth_hip.so. Nothing here falls back to torch math.
 """
+import contextlib
 import ctypes as C
 import os
 
@@ -39,10 +40,25 @@ _ws_retired = []
 _LIVE_GRAPHS = [0]
 
 
+_WS_SUFFIX = [""]
+
+
+@contextlib.contextmanager
+def workspace_scope(suffix):
+    """Every workspace requested inside the block gets its own buffer (key + suffix): calls issued
+    on a second stream then never share scratch memory with the same calls on the first."""
+    prev = _WS_SUFFIX[0]
+    _WS_SUFFIX[0] = prev + suffix
+    try:
+        yield
+    finally:
+        _WS_SUFFIX[0] = prev
+
+
 def workspace(nbytes, key="default"):
     """Reusable byte workspace on the current device (grown on demand, never shrunk)."""
     dev = torch.cuda.current_device()
-    k = (dev, key)
+    k = (dev, key + _WS_SUFFIX[0])
     buf = _ws_cache.get(k)
     if buf is None or buf.numel() < nbytes:
         if buf is not None and _LIVE_GRAPHS[0] > 0:

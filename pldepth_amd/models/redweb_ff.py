@@ -100,7 +100,13 @@ class RedWebFF:
         self.bn_prologue = int(os.environ.get("PLD_BN_PROLOGUE", "0"))
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
         self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
+        # forward: each feature-fusion layer's left branch (conv0 + bn0 + block_left: it reads
+        # only its encoder tap) on a side stream, forked as soon as the tap exists, so it runs
+        # beside the deeper encoder stages and the decoder layers above it (PLD_OVERLAP_FFL=0:
+        # one stream)
+        self.overlap_ffl = int(os.environ.get("PLD_OVERLAP_FFL", "1"))
         self._side = False
+        self._in_fside = False
         self.seed = seed
 
     preprocess = staticmethod(preprocess_input)
@@ -312,13 +318,18 @@ class RedWebFF:
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
         K.maxpool2d_fwd(A["conv1_relu"], 3, 2, 1, 1, A["pool1_pool"], self.pool_argmax)
         x = A["pool1_pool"]
+        forked = {}
         for blk in self.blocks:
             x = self._block_fwd(blk, x, training)
+            if self.overlap_ffl:
+                for d in self.ffls:
+                    if d["tap"] == blk["name"] + "out":
+                        forked[d["name"]] = self._fork_left(d, training)
         h, w = x.shape[1], x.shape[2]
         K.upsample2x_fwd(A["conv5_block3_out"], A["conv5_up"])
         up = A["conv5_up"]
         for d in self.ffls:
-            up = self._ffl_fwd(d, A[d["tap"]], up, training)
+            up = self._ffl_fwd(d, A[d["tap"]], up, training, forked.get(d["name"]))
         h, w = up.shape[1], up.shape[2]
         rows = B * h * w
         self._conv(self.aol0, up, A["aol/pre0"], h, w, h, w, bn=self.aol_bn, training=training)
@@ -394,15 +405,48 @@ class RedWebFF:
             x = A[f"{n}/out{half}"]
         return x
 
-    def _ffl_fwd(self, d, left, up, training):
+    def _ffl_left_fwd(self, d, left, training):
+        A, n = self.act, d["name"]
+        h, w = d["hw"]
+        self._conv(d["conv0"], left, A[n + "/left_pre"], h, w, h, w,
+                   bn=d["bn0"], training=training)
+        d["bn0"].apply(A[n + "/left_pre"], self.B * h * w, "none", A[n + "/left_bn"], training)
+        return self._bottleneck_fwd(d["left"], A[n + "/left_bn"], h, w, training)
+
+    def _ffl_side(self):
+        """(stream, {ffl name [+ "/bwd"]: (fork, join) events}) of the FFL left branches."""
+        if not hasattr(self, "_fside"):
+            evs = {}
+            for f in self.ffls:
+                for k in (f["name"], f["name"] + "/bwd"):
+                    evs[k] = (torch.cuda.Event(), torch.cuda.Event())
+            self._fside = (torch.cuda.Stream(device=self.device), evs)
+        return self._fside
+
+    def _fork_left(self, d, training):
+        """Run d's left branch on the FFL side stream once the main stream has produced its tap;
+        returns (left-branch output, join event). The side stream's calls use their own
+        workspaces (kernels.workspace_scope); every tensor they write belongs to the branch."""
+        stream, evs = self._ffl_side()
+        fork, join = evs[d["name"]]
+        fork.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream), K.workspace_scope("/ffl_side"):
+            stream.wait_event(fork)
+            xl = self._ffl_left_fwd(d, self.act[d["tap"]], training)
+            join.record(stream)
+        return xl, join
+
+    def _ffl_fwd(self, d, left, up, training, forked=None):
         A, n = self.act, d["name"]
         h, w = d["hw"]
         rows = self.B * h * w
-        self._conv(d["conv0"], left, A[n + "/left_pre"], h, w, h, w,
-                   bn=d["bn0"], training=training)
-        d["bn0"].apply(A[n + "/left_pre"], rows, "none", A[n + "/left_bn"], training)
-        xl = self._bottleneck_fwd(d["left"], A[n + "/left_bn"], h, w, training)
+        if forked is None:
+            xl = self._ffl_left_fwd(d, left, training)
+        else:
+            xl, join = forked
         self._conv(d["conv1"], up, A[n + "/up_pre"], h, w, h, w, bn=d["bn1"], training=training)
+        if forked is not None:
+            torch.cuda.current_stream(self.device).wait_event(join)
         d["bn1"].add_apply(A[n + "/up_pre"], rows, xl, "none", A[n + "/sum"], training)
         xd = self._bottleneck_fwd(d["down"], A[n + "/sum"], h, w, training)
         K.upsample2x_fwd(xd, A[n + "/out"])
@@ -429,7 +473,7 @@ class RedWebFF:
         args = K.conv_args(x, None, k, k, s, pt, pl, oh, ow, conv.cout,
                            math=self._math(conv, oh, ow, bwd=True))
         if conv.trainable:
-            if self._side:
+            if self._side and not self._in_fside:
                 def wg(args=args, gy=gy, rows=self.B * oh * ow, conv=conv):
                     K.conv2d_wgrad(args, gy, conv.dw)
                     if conv.db is not None:
@@ -442,7 +486,7 @@ class RedWebFF:
                     with torch.cuda.stream(wstream):
                         wstream.wait_event(fork[conv.name])
                         wg()
-            else:
+            else:  # single stream, or on the FFL side stream (already beside the main chain)
                 K.conv2d_wgrad(args, gy, conv.dw)
                 if conv.db is not None:
                     K.channel_sum(gy, self.B * oh * ow, conv.cout, conv.db)
@@ -473,11 +517,17 @@ class RedWebFF:
         self.aol_bn.bwd(A["aol/pre0"], G["aol/act0"], B * h * w, "relu", g0)
         self._wgrad_dgrad(self.aol0, A["ffl2/out"], g0, h, w, h, w, G["ffl2/out"])
         # feature fusion layers, top (ffl2) to bottom (ffl0)
+        # (with the weight-gradient overlap, each FFL's left branch runs on the FFL side stream
+        # from the moment its input gradient exists; the encoder joins it at the tap)
+        tap_join = {}
         for i in range(len(self.ffls) - 1, -1, -1):
             d = self.ffls[i]
             up = A["conv5_up"] if i == 0 else A[self.ffls[i - 1]["name"] + "/out"]
             gup = G["conv5_up"] if i == 0 else G[self.ffls[i - 1]["name"] + "/out"]
-            self._ffl_bwd(d, A[d["tap"]], G[d["tap"]], up, gup)
+            j = self._ffl_bwd(d, A[d["tap"]], G[d["tap"]], up, gup,
+                              fork=self._side and bool(self.overlap_ffl))
+            if j is not None:
+                tap_join[d["tap"]] = j
         if self._side and self._deferred:  # overlap mode 2: beside the encoder backward
             wstream, fork = self._wgrad_side()
             ev = fork[self.aol0.name]
@@ -497,10 +547,14 @@ class RedWebFF:
                 xn = "pool1_pool"
             else:
                 xn = self.blocks[bi - 1]["name"] + "out"
+            if xn in tap_join:  # this block accumulates onto the tap's decoder gradient
+                main.wait_event(tap_join.pop(xn))
             self._block_bwd(blk, A[xn], G[xn], xn in TAPS)
         hp, wp = A["pool1_pool"].shape[1:3]
         K.maxpool2d_bwd(G["pool1_pool"], self.pool_argmax, 3, 2, 1, 1, G["conv1_relu"])
         self.stem_bn.bwd(A["conv1_pre"], G["conv1_relu"], B * h * w, "relu", None)
+        for j in tap_join.values():  # (none left: every tap feeds an encoder block)
+            main.wait_event(j)
         if self._side:  # join: every weight gradient is final on the caller's stream
             main.wait_stream(self._wgrad_side()[0])
         self._side = False
@@ -551,7 +605,20 @@ class RedWebFF:
             self._wgrad_dgrad(c[half], xin, gq0, h, w, h, w, gin, gx_acc=True)
             gy = gin
 
-    def _ffl_bwd(self, d, left, gleft, up, gup):
+    def _ffl_left_bwd(self, d, left, gleft):
+        A, G, n = self.act, self.gact, d["name"]
+        h, w = d["hw"]
+        # block_left receives G[sum] unchanged (identity branch of the add)
+        self._bottleneck_bwd(d["left"], A[n + "/left_bn"], G[n + "/left_bn"], G[n + "/sum"],
+                             h, w)
+        gl = self._gpre_buf(A[n + "/left_pre"].shape, self._wslot(d["conv0"]))
+        d["bn0"].bwd(A[n + "/left_pre"], G[n + "/left_bn"], self.B * h * w, "none", gl)
+        self._wgrad_dgrad(d["conv0"], left, gl, h, w, h, w, gleft)
+
+    def _ffl_bwd(self, d, left, gleft, up, gup, fork=False):
+        """Backward of one feature-fusion layer. fork: the left branch (which needs only G[sum]
+        and writes only its own buffers, its weight gradients and the tap's gradient) runs on the
+        FFL side stream, its dW inline there; returns its join event (else None)."""
         A, G, n = self.act, self.gact, d["name"]
         h, w = d["hw"]
         rows = self.B * h * w
@@ -559,15 +626,25 @@ class RedWebFF:
         K.upsample2x_bwd(G[n + "/out"], gd)
         # block_down: input gradient lands in G[sum]; sum = bn1(up_pre) + block_left output
         self._bottleneck_bwd(d["down"], A[n + "/sum"], G[n + "/sum"], gd, h, w)
+        join = None
+        if fork:
+            stream, evs = self._ffl_side()
+            fk, join = evs[n + "/bwd"]
+            fk.record(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream), K.workspace_scope("/ffl_side"):
+                stream.wait_event(fk)
+                self._in_fside = True
+                try:
+                    self._ffl_left_bwd(d, left, gleft)
+                finally:
+                    self._in_fside = False
+                join.record(stream)
         gu = self._gpre_buf(A[n + "/up_pre"].shape, self._wslot(d["conv1"]))
         d["bn1"].bwd(A[n + "/up_pre"], G[n + "/sum"], rows, "none", gu)
         self._wgrad_dgrad(d["conv1"], up, gu, h, w, h, w, gup)
-        # block_left receives G[sum] unchanged (identity branch of the add)
-        self._bottleneck_bwd(d["left"], A[n + "/left_bn"], G[n + "/left_bn"], G[n + "/sum"],
-                             h, w)
-        gl = self._gpre_buf(A[n + "/left_pre"].shape, self._wslot(d["conv0"]))
-        d["bn0"].bwd(A[n + "/left_pre"], G[n + "/left_bn"], rows, "none", gl)
-        self._wgrad_dgrad(d["conv0"], left, gl, h, w, h, w, gleft)
+        if not fork:
+            self._ffl_left_bwd(d, left, gleft)
+        return join
 
     # ------------------------------------------------------------------ optimizer / counts
     def adam_state(self):

@@ -58,3 +58,38 @@ def test_graph_replay_equals_eager(cuda, model):
         # summation order
         bad = [k for k in sa if not torch.allclose(sa[k], sb[k], rtol=1e-4, atol=1e-6)]
         assert not bad, (i, bad[:10])
+
+
+def test_redweb_ffl_overlap_equals_single_stream(cuda, fixed_schedules):
+    """ff_redweb with the feature-fusion layers' left branches on the FFL side stream (forward
+    and backward, RedWebFF.overlap_ffl) takes the same step as with everything on one stream:
+    same kernels in the same per-stream order with the same schedules, so only the ListMLE
+    scatter-add's atomics may reorder. Eager step, then captured replays."""
+    B, H, L, R = 2, 64, 5, 20
+    rng = np.random.default_rng(1)
+    x = torch.from_numpy(rng.random((B, H, H, 3)).astype(np.float32)).to(cuda)
+    gt = torch.from_numpy(rng.random((B, H, H)).astype(np.float32)).to(cuda)
+    mask = torch.from_numpy((rng.random((B, H, H)) < 0.9).astype(np.float32)).to(cuda)
+
+    def make(overlap):
+        t = ReplicaTrainer((H, H, 3), B, L, R, 1, seed=0, model="ff_redweb")
+        t.engine.overlap_ffl = overlap
+        t.set_batch(x, gt, mask)
+        return t
+
+    a, b = make(1), make(0)
+    for t in (a, b):
+        t.step_eager(0.01)
+        t.synchronize()
+    sa, sb = _state(a), _state(b)
+    bad = [k for k in sa if not torch.allclose(sa[k], sb[k], rtol=1e-4, atol=1e-6)]
+    assert not bad, ("eager", bad[:10])
+    a.capture()
+    b.capture()
+    for i in range(3):
+        for t in (a, b):
+            t.step(0.01 * (2 + i))
+            t.synchronize()
+        sa, sb = _state(a), _state(b)
+        bad = [k for k in sa if not torch.allclose(sa[k], sb[k], rtol=1e-4, atol=1e-6)]
+        assert not bad, (i, bad[:10])
