@@ -605,7 +605,8 @@ def test_dwconv_fused_bn_swish(cuda, k, s):
 
 
 @pytest.mark.parametrize("n,h,w,c,cse", [(2, 6, 6, 96, 4), (3, 14, 14, 1152, 48),
-                                         (1, 2, 2, 16, 8)])
+                                         (1, 2, 2, 16, 8), (2, 7, 7, 240, 10),
+                                         (2, 5, 5, 672, 28)])
 def test_se_fwd_bwd(cuda, n, h, w, c, cse):
     torch.manual_seed(c)
     a = torch.randn(n, h, w, c, dtype=torch.float64, requires_grad=True)

@@ -10,5 +10,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3
 DB=$(ls $O/trace/*/run_results.db 2>/dev/null | head -1)
 [ -z "$DB" ] && DB=$(ls $O/trace/run_results.db 2>/dev/null | head -1)
 python3 $R/tools/kstats.py $DB --marker adam_amsgrad_dev_kernel --steps $STEPS --skip 1 --csv $O/kernel_stats.csv --top 60 > $O/kstats.txt
+rm -rf $O/trace
 tail -c 300 $O/bench.log
 head -45 $O/kstats.txt
