@@ -103,8 +103,10 @@ class RedWebFF:
         # forward: each feature-fusion layer's left branch (conv0 + bn0 + block_left: it reads
         # only its encoder tap) on a side stream, forked as soon as the tap exists, so it runs
         # beside the deeper encoder stages and the decoder layers above it (PLD_OVERLAP_FFL=0:
-        # one stream)
+        # one stream); PLD_OVERLAP_PROJ: the encoder's projection shortcuts (conv0 + bn0 of each
+        # stage's first block) beside conv1 -> conv2 -> conv3 in the forward
         self.overlap_ffl = int(os.environ.get("PLD_OVERLAP_FFL", "1"))
+        self.overlap_proj = int(os.environ.get("PLD_OVERLAP_PROJ", "1"))
         self._side = False
         self._in_fside = False
         self.seed = seed
@@ -343,10 +345,25 @@ class RedWebFF:
         A, B, n = self.act, self.B, blk["name"]
         h, w, oh, ow = blk["hw"]
         rows = B * oh * ow
+        join = None
         if blk["proj"]:
-            self._conv(blk["c0"], x, A[n + "0_pre"], h, w, oh, ow,
-                       bn=blk["bn0"], training=training)
-            blk["bn0"].apply(A[n + "0_pre"], rows, "none", A[n + "0_bn"], training)
+            def shortcut():
+                self._conv(blk["c0"], x, A[n + "0_pre"], h, w, oh, ow,
+                           bn=blk["bn0"], training=training)
+                blk["bn0"].apply(A[n + "0_pre"], rows, "none", A[n + "0_bn"], training)
+            if self.overlap_proj:
+                # the projection shortcut beside conv1 -> conv2 -> conv3 (joined at the add)
+                if not hasattr(self, "_pside"):
+                    self._pside = (torch.cuda.Stream(device=self.device), torch.cuda.Event(),
+                                   torch.cuda.Event())
+                stream, fork, join = self._pside
+                fork.record(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(stream), K.workspace_scope("/proj_side"):
+                    stream.wait_event(fork)
+                    shortcut()
+                    join.record(stream)
+            else:
+                shortcut()
             sc = A[n + "0_bn"]
         else:
             sc = x
@@ -377,6 +394,8 @@ class RedWebFF:
             blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
             self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
                        bn=blk["bn3"], training=training)
+        if join is not None:
+            torch.cuda.current_stream(self.device).wait_event(join)
         blk["bn3"].add_apply(A[n + "3_pre"], rows, sc, "relu", A[n + "out"], training)
         return A[n + "out"]
 

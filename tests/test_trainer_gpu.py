@@ -73,7 +73,7 @@ def test_redweb_ffl_overlap_equals_single_stream(cuda, fixed_schedules):
 
     def make(overlap):
         t = ReplicaTrainer((H, H, 3), B, L, R, 1, seed=0, model="ff_redweb")
-        t.engine.overlap_ffl = overlap
+        t.engine.overlap_ffl = t.engine.overlap_proj = overlap
         t.set_batch(x, gt, mask)
         return t
 
