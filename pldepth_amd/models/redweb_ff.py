@@ -353,10 +353,7 @@ class RedWebFF:
                 blk["bn0"].apply(A[n + "0_pre"], rows, "none", A[n + "0_bn"], training)
             if self.overlap_proj:
                 # the projection shortcut beside conv1 -> conv2 -> conv3 (joined at the add)
-                if not hasattr(self, "_pside"):
-                    self._pside = (torch.cuda.Stream(device=self.device), torch.cuda.Event(),
-                                   torch.cuda.Event())
-                stream, fork, join = self._pside
+                stream, fork, join = self._proj_side()
                 fork.record(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(stream), K.workspace_scope("/proj_side"):
                     stream.wait_event(fork)
@@ -398,6 +395,14 @@ class RedWebFF:
             torch.cuda.current_stream(self.device).wait_event(join)
         blk["bn3"].add_apply(A[n + "3_pre"], rows, sc, "relu", A[n + "out"], training)
         return A[n + "out"]
+
+    def _proj_side(self):
+        """(stream, fork, join) of the projection-shortcut branch (one branch in flight at a time:
+        each is joined inside its block)."""
+        if not hasattr(self, "_pside"):
+            self._pside = (torch.cuda.Stream(device=self.device), torch.cuda.Event(),
+                           torch.cuda.Event())
+        return self._pside
 
     def _wide(self, conv, x, h, w):
         """Whether this stride-1 1x1 conv's forward runs on the streaming wide / thin kernels
@@ -585,9 +590,24 @@ class RedWebFF:
         rows = B * oh * ow
         gout = G[n + "out"]
         g3 = self._gpre_buf(A[n + "3_pre"].shape)
+        join = None
         if blk["proj"]:
             gsc = G[n + "0_bn"]
             blk["bn3"].add_bwd(A[n + "3_pre"], gout, rows, A[n + "0_bn"], "relu", g3, gsc)
+
+            def shortcut():  # bn0 backward + conv0 dX into gx (slot 2: g3 has 0_pre's shape)
+                g0 = self._gpre_buf(A[n + "0_pre"].shape, 2)
+                blk["bn0"].bwd(A[n + "0_pre"], gsc, rows, "none", g0)
+                self._wgrad_dgrad(blk["c0"], x, g0, h, w, oh, ow, gx, gx_acc=gx_is_tap)
+            if self.overlap_proj:  # beside conv3 -> conv2 -> conv1's backward
+                stream, fork, join = self._proj_side()
+                fork.record(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(stream), K.workspace_scope("/proj_side"):
+                    stream.wait_event(fork)
+                    shortcut()
+                    join.record(stream)
+            else:
+                shortcut()
         else:
             blk["bn3"].add_bwd(A[n + "3_pre"], gout, rows, x, "relu", g3, gx,
                                dres_acc=gx_is_tap)
@@ -597,10 +617,8 @@ class RedWebFF:
         self._wgrad_dgrad(blk["c2"], A[n + "1_relu"], g2, oh, ow, oh, ow, G[n + "1_relu"])
         g1 = self._gpre_buf(A[n + "1_pre"].shape, 1)
         blk["bn1"].bwd(A[n + "1_pre"], G[n + "1_relu"], rows, "relu", g1)
-        if blk["proj"]:
-            g0 = self._gpre_buf(A[n + "0_pre"].shape)
-            blk["bn0"].bwd(A[n + "0_pre"], gsc, rows, "none", g0)
-            self._wgrad_dgrad(blk["c0"], x, g0, h, w, oh, ow, gx, gx_acc=gx_is_tap)
+        if join is not None:  # the shortcut's dX is in gx: conv1's dX accumulates onto it
+            torch.cuda.current_stream(self.device).wait_event(join)
         self._wgrad_dgrad(blk["c1"], x, g1, h, w, oh, ow, gx, gx_acc=True)
 
     def _bottleneck_bwd(self, bt, x, gx, gy, h, w):
