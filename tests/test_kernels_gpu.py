@@ -377,6 +377,8 @@ def test_channel_sum(cuda):
 # ------------------------------------------------------------------------------------ BN
 @pytest.mark.parametrize("rows,c,act", [(4096, 32, "relu"), (999, 144, "swish"),
                                         (300, 1280, "swish"), (50, 6, "none"),
+                                        # two channel columns of 84 groups (red_plan)
+                                        (3001, 672, "swish"),
                                         # grid-stride apply loops (> 8192 x 256 vectors): the
                                         # grid is a multiple of C / VW groups per thread
                                         (100003, 96, "swish"), (2100007, 3, "relu")])
