@@ -28,6 +28,11 @@ KIND_PEAK = {0: FP32_MFMA_PEAK_TFLOPS, 1: BF16_MFMA_PEAK_TFLOPS / 3.0, 2: FP32_M
 KIND_NAME = {0: "fp32_mfma", 1: "bf16x3_mfma", 2: "direct_valu"}
 
 
+def log(msg):
+    """progress on stderr (stdout carries only rank 0's JSON line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def synthetic_batch(B, H, W, seed):
     """x ~ U[0,1); gt = smooth 8-bit-quantised depth field; mask ~ Bernoulli(0.9)."""
     rng = np.random.default_rng(seed)
@@ -174,7 +179,8 @@ def step_byte_floor(trainer, lr):
              and getattr(f, "__module__", None) == K.__name__ and n not in (
                  "ptr", "stream", "workspace", "conv_args", "conv_policy", "encoder_math",
                  "set_conv_math", "same_pads", "sampler_candidates", "pgemm_ok", "pgemm_pays",
-                 "load_tile_cache", "save_tile_cache", "Graph")]
+                 "load_tile_cache", "save_tile_cache", "Graph", "schedule_desc",
+                 "use_schedule_table")]
     saved = {n: getattr(K, n) for n in names}
 
     def wrap(n, f):
@@ -481,9 +487,11 @@ def run_config(model, H, B, L, R, sampling_type, steps, warmup, rank, world, pg,
     tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
                  torch.from_numpy(mask).cuda())
     lr = 0.01
+    log(f"{model} {H}x{H} B={B} L={L} R={R}: first (eager) step")
     tr.step_eager(lr)
     torch.cuda.synchronize()
     if graph:
+        log("capture")
         tr.capture()
     for _ in range(max(warmup - 1, 0)):
         tr.step(lr)
@@ -516,6 +524,30 @@ EXTRA_CONFIGS = [
     ("cfg3_ff_resnet", "ff_redweb", 5, 100),
     ("cfg5_ff_effnet_L64_R1000", "ff_effnet", 64, 1000),
 ]
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): run
+    the N ranks as ONE child process, `torch.distributed.run --nproc-per-node N` on 127.0.0.1
+    (each rank pins LOCAL_RANK to its GPU), and return its exit code. The parent never touches
+    the GPU (no HIP call before or after), it only waits; rank 0's JSON line reaches stdout
+    through the child."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -554,10 +586,17 @@ def main():
     ap.add_argument("--step-traffic-profile", default="profiles/r03_pmc_step_family.json",
                     help="PMC HBM bytes of one eager step per op family "
                          "(tools/pmc_step_family.py): roofline.step_bytes_measured")
-    ap.add_argument("--tile-cache", default="",
-                    help="JSON of tuned conv schedules: loaded if present, written after tuning")
+    ap.add_argument("--schedules", default="",
+                    help="persisted conv schedule table (default: pldepth_amd/schedules/"
+                         "gfx950.json): every conv schedule fixed before the first step, no "
+                         "timing-dependent choice in the run")
+    ap.add_argument("--tune", default="",
+                    help="autotune the schedules by timing instead (each candidate timed alone "
+                         "on a drained device) and write the table to this path")
     a = ap.parse_args()
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -575,24 +614,30 @@ def main():
         else:
             dist.init_process_group(a.backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
+    # what the process group actually holds (the SCALE record shows RCCL saw N ranks)
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    backend_seen = str(dist.get_backend()) if world > 1 else None
 
     from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
     from pldepth_amd import kernels as K
     K.set_conv_math(a.conv_math)
-    if a.tile_cache and os.path.exists(a.tile_cache):
-        K.load_tile_cache(a.tile_cache)
+    sched = {"mode": "tuned in this run"}
+    path = a.schedules or K.DEFAULT_SCHEDULES
+    if not a.tune and os.path.exists(path):
+        n_sched, sha = K.use_schedule_table(path)
+        sched = {"mode": "table", "table": os.path.relpath(path, ROOT), "sha1": sha,
+                 "entries": n_sched}
 
     H = a.size
     B, L, R = a.batch, a.ranking_size, a.rankings_per_image
     tr, elapsed = run_config(a.model, H, B, L, R, a.sampling_type, a.steps, a.warmup, rank,
                              world, pg, graph=not a.no_graph)
-    if a.tile_cache and rank == 0:
-        K.save_tile_cache(a.tile_cache)
     loss = tr.loss_value()
     value = world * B * a.steps / elapsed
 
     # dominant conv kernel + conv family: algorithmic FLOPs / measured duration (HIP events on
     # the trainer's stream, one eager step)
+    log(f"timed: {1e3 * elapsed / a.steps:.3f} ms/step; profiling")
     recs = profile_conv(tr, 0.01)
     flops_img = tr.engine.conv_flops_per_image()
     roof = conv_roofline(recs, a.traffic_profile)
@@ -625,13 +670,16 @@ def main():
                    "model": a.model, "global_batch": world * B, "input": f"{H}x{H}",
                    "ranking_size": L, "rankings_per_image": R,
                    "parallelism": f"dp{world}", "graph": not a.no_graph,
-                   "backend": a.backend if world > 1 else None},
+                   "backend": backend_seen, "ranks_seen": ranks_seen,
+                   "gpus_visible": torch.cuda.device_count()},
         "conv_math": {"policy": a.conv_math, "encoder": tr.engine.enc_math,
                       "decoder": tr.engine.dec_math},
         "roofline": roof,
         "loss": loss,
+        "schedules": sched,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.no_loss_parity:
+        log("loss parity vs the fp64 oracle")
         par = loss_parity(tr, 0.01)
         out["loss_delta"] = par["loss_delta"]
         out["loss_parity"] = par
@@ -649,7 +697,11 @@ def main():
             del t2
             torch.cuda.empty_cache()
         out["extra_configs"] = extra
+    if a.tune and rank == 0:
+        K.save_tile_cache(a.tune)
+        out["schedules"]["written"] = a.tune
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(H, H, L, R, a.model)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -143,6 +143,11 @@ int pld_conv_num_schedules(int math);
 enum { PLD_SCHED_X3 = 0, PLD_SCHED_X3_SPLIT = 1, PLD_SCHED_X3_PATCH = 2, PLD_SCHED_FP32 = 3,
        PLD_SCHED_FP32_SPLIT = 4 };
 int pld_conv_schedule_class(int math, int idx);
+/* a stable text name of schedule `idx` ("x3/128x128", "x3split/256x64", "x3patch/32",
+ * "fp32/128x96", "fp32split/256x32"; NULL if out of range): a persisted tuning table keys its
+ * choices by this name, so it stays valid across library builds whose schedule tables keep
+ * the same entries (bench.py / pldepth_amd/schedules/). */
+const char* pld_conv_schedule_desc(int math, int idx);
 /* which kernel family a conv call runs (mode 0 = fwd, 1 = dgrad, 2 = wgrad) for its math and
  * tile: PLD_KIND_FP32 (v_mfma_f32_32x32x2_f32), PLD_KIND_BF16X3 (v_mfma_f32_32x32x16_bf16 x3) or
  * PLD_KIND_DIRECT (VALU kernels: single-output-channel 3x3 convs, thin 1x1 convs with GEMM K <= 48,

@@ -56,6 +56,7 @@ _SIGS = {
                                       P]),
     "pld_conv_num_schedules": (I32, [I32]),
     "pld_conv_schedule_class": (I32, [I32, I32]),
+    "pld_conv_schedule_desc": (C.c_char_p, [I32, I32]),
     "pld_conv_kernel_kind": (I32, [C.POINTER(ConvArgs), I32]),
     "pld_conv_kernel_name": (C.c_char_p, [C.POINTER(ConvArgs), I32]),
     "pld_conv2d_fwd_workspace_size": (SZ, [C.POINTER(ConvArgs)]),
@@ -132,7 +133,7 @@ _SIGS = {
 
 # functions returning a value rather than a status
 _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_tiles", "pld_conv_num_schedules",
-               "pld_conv_schedule_class",
+               "pld_conv_schedule_class", "pld_conv_schedule_desc",
                "pld_conv_kernel_kind", "pld_conv_kernel_name",
                "pld_conv2d_fwd_workspace_size", "pld_conv2d_dgrad_workspace_size", "pld_conv2d_wgrad_workspace_size",
                "pld_conv2d_fwd_bn_stats_workspace_size",

@@ -22,6 +22,7 @@
 // Roofline: MFMA-bound for the decoder shapes (fp32 peak 157.3 TF/s), HBM-bound for skinny
 // encoder 1x1 convs (K = 16..40).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "conv_common.h"
@@ -817,6 +818,7 @@ extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
 extern "C" int pld__x3_num_patch(void);
+extern "C" int pld__x3_patch_bn(int cfg);
 extern "C" int pld__x3_patch_ok(const GemmConvParams* p, int cfg);
 extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream);
 extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
@@ -1222,6 +1224,33 @@ extern "C" int pld_conv_schedule_class(int math, int idx) {
   if (idx < 2 * n3) return PLD_SCHED_X3_SPLIT;
   if (idx < nx) return PLD_SCHED_X3_PATCH;
   return idx - nx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
+}
+
+extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
+  // one slot per schedule index and math, written once (the tables are constant)
+  static char names[2][128][24];
+  const int cls = pld_conv_schedule_class(math, idx);
+  if (cls < 0 || idx >= 128) return nullptr;
+  char* out = names[math == PLD_MATH_BF16X3 ? 1 : 0][idx];
+  if (out[0]) return out;
+  const int n3 = pld__x3_num_cfg();
+  const int nx = math == PLD_MATH_BF16X3 ? 2 * n3 + pld__x3_num_patch() : 0;
+  int bm = 0, bn = 0, tm, tn, occ;
+  switch (cls) {
+    case PLD_SCHED_X3:
+    case PLD_SCHED_X3_SPLIT:
+      pld__x3_cfg_dims(idx % n3, &bm, &bn, &tm, &tn, &occ);
+      snprintf(out, 24, "%s/%dx%d", cls == PLD_SCHED_X3 ? "x3" : "x3split", bm, bn);
+      break;
+    case PLD_SCHED_X3_PATCH:
+      snprintf(out, 24, "x3patch/%d", pld__x3_patch_bn(idx - 2 * n3));
+      break;
+    default: {
+      const TileCfg& t = kTiles[(idx - nx) % kNumCfg];
+      snprintf(out, 24, "%s/%dx%d", cls == PLD_SCHED_FP32 ? "fp32" : "fp32split", t.bm, t.bn);
+    }
+  }
+  return out;
 }
 
 extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {

@@ -685,148 +685,13 @@ __global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
   }
 }
 
-// The same for inputs of several 32-channel chunks (C % 16 == 0 per source; a concat's sources
-// chunked separately, a ragged 16-channel chunk masked): 32 output channels per workgroup, the
-// (patch, filter) stage of chunk i+1 loaded into registers while chunk i is multiplied, double
-// buffered in LDS (2 x 80 KB).
+// Inputs of several 32-channel chunks (C % 16 == 0 per source; a concat's sources chunked
+// separately, a ragged 16-channel chunk masked): 32 output channels per workgroup, one (patch,
+// filter) stage per chunk, double buffered in LDS (2 x 80 KB).
 constexpr int MC_STAGE = 2 * PatchSmem<32>::A_PLANE + 2 * PatchSmem<32>::B_PLANE;
 
-template <bool CAT>
-__global__ __launch_bounds__(512) void conv_x3_patch_mc_kernel(GemmConvParams p) {
-  using S = PatchSmem<32>;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * MC_STAGE];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
-  const int nwg = gridDim.x * gridDim.y;
-  const int flat = blockIdx.x + gridDim.x * blockIdx.y;
-  const int xcd = flat & 7, slot = flat >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int nb = wid % gridDim.y;
-  int t = wid / gridDim.y;
-  const int tx0 = t % tiles_x;
-  t /= tiles_x;
-  const int ty0 = t % tiles_y;
-  const int img = t / tiles_y;
-  const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W, n0 = nb * 32;
-  const int nch = p.kc_tap;  // chunks: kc1 of x1, then those of x2
-  const long img1 = (long)p.h * p.w * p.c1, img2 = (long)p.h * p.w * p.c2;
-  const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.x1 + img * img1, img1 * 4);
-  const __amdgpu_buffer_rsrc_t rs2 = CAT ? make_rsrc(p.x2 + img * img2, img2 * 4) : rs1;
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.bsplit, (long)p.N * p.K * 4);
-
-  constexpr int EA = P_PIX * 8, IA = (EA + 511) / 512;
-  constexpr int EB = 9 * 32 * 8, IB = (EB + 511) / 512;
-  float4 va[IA], vb[IB];
-  auto load = [&](int ch) {
-    ch = min(ch, nch - 1);
-    const bool s2 = CAT && ch >= p.kc1;
-    const int cb = (s2 ? ch - p.kc1 : ch) * 32, cs = s2 ? p.c2 : p.c1;
-    const __amdgpu_buffer_rsrc_t rs = s2 ? rs2 : rs1;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      const int px = e >> 3, c4 = (e & 7) * 4;
-      const int py = px / P_W, pxx = px - py * P_W;
-      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
-      const bool ok = e < EA && cb + c4 < cs && (unsigned)iy < (unsigned)p.h &&
-                      (unsigned)ix < (unsigned)p.w;
-      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
-    }
-    const int kb = (s2 ? p.c1 : 0) + cb;  // chunk's first channel in the filter's k = tap C + ci
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
-      const int tap = nt >> 5, n = nt & 31;
-      const bool ok = e < EB && n0 + n < p.N && cb + 8 * c < cs;
-      vb[i] = bload4(rb, ok ? (unsigned)(((n0 + n) * p.K + tap * p.C + kb + 8 * c) * 4 + 16 * half)
-                            : OOB);
-    }
-  };
-  auto store = [&](int buf) {
-    unsigned char* Ah = smem + buf * MC_STAGE;
-    unsigned char* Al = Ah + S::A_PLANE;
-    unsigned char* Bh = Ah + 2 * S::A_PLANE;
-    unsigned char* Bl = Bh + S::B_PLANE;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      if (e < EA) {
-        const int px = e >> 3, q = e & 7;
-        unsigned h0, l0, h1, l1;
-        split2(va[i].x, va[i].y, h0, l0);
-        split2(va[i].z, va[i].w, h1, l1);
-        const int o = chunk_off(px, q >> 1) + 8 * (q & 1);
-        *reinterpret_cast<u32x2*>(Ah + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(Al + o) = u32x2{l0, l1};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      if (e < EB) {
-        const int half = e & 1, c = (e >> 1) & 3, nt = e >> 3;
-        const int tap = nt >> 5, n = nt & 31;
-        *reinterpret_cast<float4*>((half ? Bl : Bh) + tap * S::B_TAP + chunk_off(n, c)) = vb[i];
-      }
-    }
-  };
-
-  const int h = lane >> 5, l32 = lane & 31;
-  floatx16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
-    const int buf = ch & 1;
-    load(ch + 1);
-    const unsigned char* Ah = smem + buf * MC_STAGE;
-    const unsigned char* Al = Ah + S::A_PLANE;
-    const unsigned char* Bh = Ah + 2 * S::A_PLANE;
-    const unsigned char* Bl = Bh + S::B_PLANE;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int r = (wave + tap / 3) * P_W + l32 + tap % 3;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 ah = lds_frag(Ah, r, 2 * s + h), al = lds_frag(Al, r, 2 * s + h);
-        const bf16x8 bh = lds_frag(Bh + tap * S::B_TAP, l32, 2 * s + h);
-        const bf16x8 bl = lds_frag(Bl + tap * S::B_TAP, l32, 2 * s + h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-      }
-    }
-    if (ch + 1 < nch) store(buf ^ 1);
-    __syncthreads();
-  }
-
-  const int oy = oy0 + wave;
-  const int col = n0 + l32;
-  if (oy >= p.oh || col >= p.N) return;
-  const float bias = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int ox = ox0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (ox >= p.ow) continue;
-    const long row = ((long)img * p.oh + oy) * p.ow + ox;
-    const float v = acc[r] + bias;
-    if (col < p.split) {
-      float* dst = p.out1 + row * p.ld1 + col;
-      *dst = p.acc1 ? *dst + v : v;
-    } else {
-      float* dst = p.out2 + row * p.ld2 + (col - p.split);
-      *dst = p.acc2 ? *dst + v : v;
-    }
-  }
-}
-
-// The multi-chunk patch conv, warp-specialised (round 3; the pattern of
-// conv_x3_patch_wgrad_pc_kernel): waves 0-3 compute two output rows each (2 accumulators, the
+// The multi-chunk patch conv, warp-specialised (the pattern of conv_x3_patch_wgrad_pc_kernel):
+// waves 0-3 compute two output rows each (2 accumulators, the
 // filter fragments of a (tap, k-half) shared by both rows, the next fragments read while the
 // current ones multiply), waves 4-7 stage the next chunk (global loads one chunk ahead in
 // registers, patch hi/lo split, pre-split filter copied) into the other LDS buffer. One barrier
@@ -1007,11 +872,9 @@ constexpr int kNumPatch = 3;
 // workgroup owns one 32-channel chunk of ONE source (all 9 taps: 9 MFMA row tiles) x 32 output
 // channels, and loops over a range of 8 x 32-pixel output tiles (its split-K share). Per tile it
 // stages the 10 x 34 input patch of the chunk and the 256 x 32 dY tile as [pixel][channel] hi/lo
-// images, double-buffered; each of the 8 waves takes one output row (two 16-pixel k-steps) and
-// accumulates all 9 taps — the A fragment of tap (ty, tx) is the patch image read transposed
+// images, double-buffered; the A fragment of tap (ty, tx) is the patch image read transposed
 // (ds_read_b64_tr_b16) from row (row + ty) * 34 + tx on, the dY fragment is shared by the 9
-// taps. Every input value is staged once per tile, not once per tap. The 8 waves' partial sums
-// are combined in LDS by a fixed tree at the end (deterministic).
+// taps. Every input value is staged once per tile, not once per tap.
 constexpr int PW_A = P_PIX * 64;       // patch image plane: [340 pixels][32 ch] bf16
 constexpr int PW_B = PT_H * PT_W * 64; // dY image plane: [256 pixels][32 co] bf16
 constexpr int PW_STAGE = 2 * PW_A + 2 * PW_B;
@@ -1029,150 +892,9 @@ __device__ __forceinline__ bf16x8 tr_frag_rows(const unsigned char* plane, int r
   return __builtin_bit_cast(bf16x8, v);
 }
 
-__global__ __launch_bounds__(512) void conv_x3_patch_wgrad_kernel(GemmConvParams p, int tiles,
-                                                                  int tiles_per_split) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PW_STAGE];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
-  const bool s2 = q >= p.kc1;
-  const int cb = (s2 ? q - p.kc1 : q) * 32;  // first channel of the chunk in its source
-  const int cs = s2 ? p.c2 : p.c1;
-  const int nv = min(32, cs - cb);           // valid channels of the chunk
-  const int n0 = nb * 32;
-  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
-  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
-  const long img_in = (long)p.h * p.w * cs;
-  const float* xsrc = s2 ? p.x2 : p.x1;
-
-  constexpr int EA = P_PIX * 8, IA = (EA + 511) / 512;  // patch: 4-channel quads
-  constexpr int EB = PT_H * PT_W * 8, IB = EB / 512;    // dY: 4-channel quads
-  float4 va[IA], vb[IB];
-  auto load = [&](int t) {
-    t = min(t, t_end - 1);  // past the end: a harmless re-load of the last tile
-    const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
-    const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      const int px = e >> 3, c4 = (e & 7) * 4;
-      const int py = px / P_W, pxx = px - py * P_W;
-      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
-      const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
-                      (unsigned)ix < (unsigned)p.w;
-      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
-    }
-    const long img_out = (long)p.oh * p.ow;
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      const int k = e >> 3, c4 = (e & 7) * 4;
-      const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
-      const bool ok = oy < p.oh && ox < p.ow && n0 + c4 < p.N;
-      vb[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
-    }
-  };
-  auto store = [&](int buf) {
-    unsigned char* A = smem + buf * PW_STAGE;
-    unsigned char* B = A + 2 * PW_A;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      if (e < EA) {
-        unsigned h0, l0, h1, l1;
-        split2(va[i].x, va[i].y, h0, l0);
-        split2(va[i].z, va[i].w, h1, l1);
-        const int o = (e >> 3) * 64 + (e & 7) * 8;
-        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(A + PW_A + o) = u32x2{l0, l1};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + 512 * i;
-      unsigned h0, l0, h1, l1;
-      split2(vb[i].x, vb[i].y, h0, l0);
-      split2(vb[i].z, vb[i].w, h1, l1);
-      const int o = (e >> 3) * 64 + (e & 7) * 8;
-      *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
-      *reinterpret_cast<u32x2*>(B + PW_B + o) = u32x2{l0, l1};
-    }
-  };
-
-  floatx16 acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  if (t_begin < t_end) {
-    load(t_begin);
-    store(0);
-    __syncthreads();
-    for (int t = t_begin; t < t_end; ++t) {
-      const int buf = (t - t_begin) & 1;
-      load(t + 1);
-      const unsigned char* A = smem + buf * PW_STAGE;
-      const unsigned char* B = A + 2 * PW_A;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int k0 = 32 * wave + 16 * s;  // this wave's 16 output pixels (row `wave`)
-        const bf16x8 bh = tr_frag_rows(B, k0, lane), bl = tr_frag_rows(B + PW_B, k0, lane);
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int r0 = (wave + tap / 3) * P_W + 16 * s + tap % 3;
-          const bf16x8 ah = tr_frag_rows(A, r0, lane), al = tr_frag_rows(A + PW_A, r0, lane);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
-          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
-        }
-      }
-      if (t + 1 < t_end) store(buf ^ 1);
-      __syncthreads();
-    }
-  }
-  // combine the 8 waves: 4 -> 0..3, 2 -> 0..1, 1 -> 0 through LDS (fixed tree)
-  float* red = reinterpret_cast<float*>(smem);  // 4 slots x 9 tiles x 64 lanes x 16
-  for (int half = 4; half >= 1; half >>= 1) {
-    if (wave >= half && wave < 2 * half) {
-      float* slot = red + (long)(wave - half) * 9 * 64 * 16;
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) slot[(t * 16 + r) * 64 + lane] = acc[t][r];
-    }
-    __syncthreads();
-    if (wave < half) {
-      const float* slot = red + (long)wave * 9 * 64 * 16;
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] += slot[(t * 16 + r) * 64 + lane];
-    }
-    __syncthreads();
-  }
-  if (wave != 0) return;
-  const int h = lane >> 5, col = n0 + (lane & 31);
-  if (col >= p.N) return;
-  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (ci >= nv) continue;
-      const long m = (long)t * p.C + (s2 ? p.c1 : 0) + cb + ci;
-      float* dst = out + m * p.N + col;
-      *dst = (p.zstride == 0 && p.acc1) ? *dst + acc[t][r] : acc[t][r];
-    }
-}
-
-// The same contraction, warp-specialised (round 3). The uniform kernel above holds 9 accumulator
-// tiles (144 VGPRs) + the next tile's loads in every wave at 2 waves per SIMD, which leaves one
-// fragment register set: every MFMA pair waits on its own transposed LDS read (lgkmcnt(0)),
-// and all waves split + store the next tile together while the matrix pipes idle (MFMA 31 %
-// busy). Here waves 0-3 only compute — wave c owns output rows 2c, 2c+1 of the 8 x 32 tile (four
+// Warp-specialised (round 3; a uniform-role form, where every wave holds 9 accumulator tiles +
+// the next tile's loads, left the matrix pipes idle while all waves split and stored: MFMA 31 %
+// busy). Waves 0-3 only compute — wave c owns output rows 2c, 2c+1 of the 8 x 32 tile (four
 // 16-pixel k-steps, all 9 taps), with the next tap's A fragments and the next k-step's dY
 // fragments read while the current ones multiply — and waves 4-7 only stage: global loads two
 // tiles ahead in registers, bf16 hi/lo split, LDS stores into the other buffer. One barrier per
@@ -1355,22 +1077,10 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad_pc_kernel(GemmConvPar
   }
 }
 
-// The same for 64 output channels per workgroup (N > 32: the 240- and 144-wide decoder convs):
-// the input patch of a tile is staged ONCE for both 32-wide cout tiles (the 32-wide kernel
-// re-stages it per cout tile: 8 / 5 times for N = 240 / 144 — fetch-bound, PMC: 2.9x the
-// algorithmic bytes). 768 threads = 12 waves = 2 cout tiles x 3 tap rows (ty) x 2 row halves:
-// a wave accumulates the 3 taps (ty, 0..2) of one cout tile over 4 output rows (8 pixel
-// k-steps): 48 accumulator VGPRs, 3 waves per SIMD. One LDS stage (patch 43.5 KB + the
-// [256 px][64 co] dY image 64 KB) with the next tile's global loads held in registers during the
-// MFMAs. dY rows are 128 B: the 32-byte column blocks are XOR-swizzled by 2 ((row >> 1) & 1) so
-// the transposed reads of 4 consecutive rows hit 4 distinct bank ranges. The two row halves are
-// summed through LDS at the end (fixed order).
-constexpr int PW_B64 = PT_H * PT_W * 128;     // dY image plane: [256 pixels][64 co] bf16
-constexpr int PW64_STAGE = 2 * PW_A + 2 * PW_B64;
-constexpr int PW64_RED = 6 * 3 * 64 * 16 * 4;   // 6 slots of 3 tiles x 64 lanes x 16 floats
-constexpr int PW64_SMEM = PW64_STAGE > PW64_RED ? PW64_STAGE : PW64_RED;
-constexpr int PW64_T = 768;
-
+// 64 output channels per workgroup (N > 32): the input patch of a tile is staged ONCE for both
+// 32-wide cout tiles (the 32-wide kernel re-stages it per cout tile: fetch-bound, PMC 2.9x the
+// algorithmic bytes for N = 240). dY rows are 128 B: the 32-byte column blocks are XOR-swizzled
+// by 2 ((row >> 1) & 1) so the transposed reads of 4 consecutive rows hit 4 distinct bank ranges.
 __device__ __forceinline__ int dy64_off(int k, int col) {  // byte offset of (row k, cout col)
   return k * 128 + (((col >> 4) ^ (((k >> 1) & 1) << 1)) << 5) + (col & 15) * 2;
 }
@@ -1385,146 +1095,6 @@ __device__ __forceinline__ bf16x8 tr_frag_dy64(const unsigned char* plane, int r
       __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plane + dy64_off(r + 4, col)));
   const v4s v[2] = {lo, hi};
   return __builtin_bit_cast(bf16x8, v);
-}
-
-__global__ __launch_bounds__(PW64_T) void conv_x3_patch_wgrad64_kernel(GemmConvParams p,
-                                                                       int tiles,
-                                                                       int tiles_per_split) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[PW64_SMEM];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
-  const bool s2 = q >= p.kc1;
-  const int cb = (s2 ? q - p.kc1 : q) * 32;
-  const int cs = s2 ? p.c2 : p.c1;
-  const int nv = min(32, cs - cb);
-  const int n0 = nb * 64;
-  const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
-  const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
-  const long img_in = (long)p.h * p.w * cs;
-  const float* xsrc = s2 ? p.x2 : p.x1;
-  unsigned char* A = smem;
-  unsigned char* B = smem + 2 * PW_A;
-
-  constexpr int EA = P_PIX * 8, IA = (EA + PW64_T - 1) / PW64_T;    // patch: 4-channel quads
-  constexpr int EB = PT_H * PT_W * 16, IB = (EB + PW64_T - 1) / PW64_T;  // dY: 4-cout quads
-  float4 va[IA], vb[IB];
-  auto load = [&](int t) {
-    const int tx0 = t % tiles_x, r1 = t / tiles_x, ty0 = r1 % tiles_y, img = r1 / tiles_y;
-    const int oy0 = ty0 * PT_H, ox0 = tx0 * PT_W;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(xsrc + img * img_in, img_in * 4);
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + PW64_T * i;
-      const int px = e >> 3, c4 = (e & 7) * 4;
-      const int py = px / P_W, pxx = px - py * P_W;
-      const int iy = oy0 - p.pt + py, ix = ox0 - p.pl + pxx;
-      const bool ok = e < EA && c4 < nv && (unsigned)iy < (unsigned)p.h &&
-                      (unsigned)ix < (unsigned)p.w;
-      va[i] = bload4(rs, ok ? (unsigned)(((iy * p.w + ix) * cs + cb + c4) * 4) : OOB);
-    }
-    const long img_out = (long)p.oh * p.ow;
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.bmat + img * img_out * p.N, img_out * p.N * 4);
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + PW64_T * i;
-      const int k = e >> 4, c4 = (e & 15) * 4;
-      const int oy = oy0 + (k >> 5), ox = ox0 + (k & 31);
-      const bool ok = e < EB && oy < p.oh && ox < p.ow && n0 + c4 < p.N;
-      vb[i] = bload4(rd, ok ? (unsigned)(((oy * p.ow + ox) * p.N + n0 + c4) * 4) : OOB);
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      const int e = threadIdx.x + PW64_T * i;
-      if (e < EA) {
-        unsigned h0, l0, h1, l1;
-        split2(va[i].x, va[i].y, h0, l0);
-        split2(va[i].z, va[i].w, h1, l1);
-        const int o = (e >> 3) * 64 + (e & 7) * 8;
-        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(A + PW_A + o) = u32x2{l0, l1};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int e = threadIdx.x + PW64_T * i;
-      if (e < EB) {
-        unsigned h0, l0, h1, l1;
-        split2(vb[i].x, vb[i].y, h0, l0);
-        split2(vb[i].z, vb[i].w, h1, l1);
-        const int o = dy64_off(e >> 4, (e & 15) * 4);
-        *reinterpret_cast<u32x2*>(B + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(B + PW_B64 + o) = u32x2{l0, l1};
-      }
-    }
-  };
-
-  const int ct = wave / 6, ty = (wave % 6) >> 1, rh = wave & 1;
-  floatx16 acc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  if (t_begin < t_end) {
-    load(t_begin);
-    store();
-    __syncthreads();
-    for (int t = t_begin; t < t_end; ++t) {
-      if (t + 1 < t_end) load(t + 1);  // in flight under the MFMAs
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 4 * rh + rr;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int k0 = 32 * row + 16 * s;
-          const bf16x8 bh = tr_frag_dy64(B, k0, 32 * ct, lane);
-          const bf16x8 bl = tr_frag_dy64(B + PW_B64, k0, 32 * ct, lane);
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) {
-            const int r0 = (row + ty) * P_W + 16 * s + tx;
-            const bf16x8 ah = tr_frag_rows(A, r0, lane), al = tr_frag_rows(A + PW_A, r0, lane);
-            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tx], 0, 0, 0);
-            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tx], 0, 0, 0);
-            acc[tx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tx], 0, 0, 0);
-          }
-        }
-      }
-      __syncthreads();  // every wave is done with this tile's LDS
-      if (t + 1 < t_end) {
-        store();
-        __syncthreads();
-      }
-    }
-  }
-  // the two row halves of each (cout tile, tap row): rh 1 -> rh 0 through LDS
-  float* slot = reinterpret_cast<float*>(smem) + (long)(wave >> 1) * 3 * 64 * 16;
-  if (rh == 1) {
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) slot[(t * 16 + r) * 64 + lane] = acc[t][r];
-  }
-  __syncthreads();
-  if (rh == 1) return;
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] += slot[(t * 16 + r) * 64 + lane];
-  const int h = lane >> 5, col = n0 + 32 * ct + (lane & 31);
-  if (col >= p.N) return;
-  float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
-#pragma unroll
-  for (int tx = 0; tx < 3; ++tx)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (ci >= nv) continue;
-      const long m = (long)(ty * 3 + tx) * p.C + (s2 ? p.c1 : 0) + cb + ci;
-      float* dst = out + m * p.N + col;
-      *dst = (p.zstride == 0 && p.acc1) ? *dst + acc[tx][r] : acc[tx][r];
-    }
 }
 
 // The 64-cout weight gradient in the producer/consumer form of conv_x3_patch_wgrad_pc_kernel.
@@ -1839,15 +1409,9 @@ extern "C" int pld__x3_patch_launch(GemmConvParams* p, int cfg, void* stream) {
     p->kc1 = (int)cdiv(p->c1, 32);
     p->kc_tap = p->kc1 + (int)cdiv(p->c2, 32);
     dim3 grid(tiles, cdiv(p->N, 32));
-#ifdef X3_MC_UNIFORM  // the round-2 uniform-role kernel (A/B builds only)
-    if (p->c2) x3::conv_x3_patch_mc_kernel<true><<<grid, 512, 0, as_stream(stream)>>>(*p);
-    else x3::conv_x3_patch_mc_kernel<false><<<grid, 512, 0, as_stream(stream)>>>(*p);
-    return check_launch("conv_x3_patch_mc_kernel");
-#else
     if (p->c2) x3::conv_x3_patch_mc_pc_kernel<true><<<grid, 512, 0, as_stream(stream)>>>(*p);
     else x3::conv_x3_patch_mc_pc_kernel<false><<<grid, 512, 0, as_stream(stream)>>>(*p);
     return check_launch("conv_x3_patch_mc_pc_kernel");
-#endif
   }
   const int bn = x3::kPatchBN[cfg];
   dim3 grid(tiles, cdiv(p->N, bn));
@@ -1874,11 +1438,7 @@ extern "C" int pld__x3_patch_wgrad_cw(int N) {
 }
 // output rows per tile: 8, or 4 for the double-buffered 64-cout kernel
 extern "C" int pld__x3_patch_wgrad_th(int N) {
-#ifdef X3_PW64_SINGLE  // the round-2 single-stage 64-cout kernel (A/B builds only)
-  return x3::PT_H;
-#else
   return pld__x3_patch_wgrad_cw(N) == 64 ? x3::Q_H : x3::PT_H;
-#endif
 }
 extern "C" int pld__x3_patch_wgrad_tiles(const GemmConvParams* p) {
   return (int)(cdiv(p->ow, x3::PT_W) * cdiv(p->oh, pld__x3_patch_wgrad_th(p->N)) * p->n);
@@ -1895,22 +1455,12 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
   const int chunks = p->kc1 + (int)cdiv(p->c2, 32);
   if (pld__x3_patch_wgrad_cw(p->N) == 64) {
     dim3 grid(chunks, cdiv(p->N, 64), cdiv(tiles, tps));
-#ifdef X3_PW64_SINGLE
-    x3::conv_x3_patch_wgrad64_kernel<<<grid, x3::PW64_T, 0, as_stream(stream)>>>(*p, tiles, tps);
-    return check_launch("conv_x3_patch_wgrad64_kernel");
-#else
     x3::conv_x3_patch_wgrad64_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
     return check_launch("conv_x3_patch_wgrad64_pc_kernel");
-#endif
   }
   dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
-#ifdef X3_PW_UNIFORM  // the round-2 uniform-role kernel (A/B builds only)
-  x3::conv_x3_patch_wgrad_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
-  return check_launch("conv_x3_patch_wgrad_kernel");
-#else
   x3::conv_x3_patch_wgrad_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
   return check_launch("conv_x3_patch_wgrad_pc_kernel");
-#endif
 }
 extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {

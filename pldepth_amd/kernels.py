@@ -258,45 +258,84 @@ _TILE_CACHE = {}
 _CAPTURING = [False]
 
 
-def _tile_cache_meta():
-    """What a tuned schedule index means depends on the schedule tables of THIS library build
-    and on the GPU: a cache from another build / arch is ignored."""
-    import hashlib
-    from ._lib import LIB_PATH
-    h = hashlib.sha1()
-    with open(LIB_PATH, "rb") as f:
-        for blk in iter(lambda: f.read(1 << 20), b""):
-            h.update(blk)
-    arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName \
+# The persisted schedule table of the bench workloads on MI355X (written by
+# `bench.py --tune`, loaded by default by bench.py and by the parity tests of the bench's
+# arithmetic): with it every conv schedule of a run is fixed before the first step, no choice
+# depends on timing, and the same table governs the timed run and its gradient checks.
+DEFAULT_SCHEDULES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "schedules",
+                                 "gfx950.json")
+SCHEDULE_FORMAT = 2
+
+
+def _arch():
+    return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName \
         if torch.cuda.is_available() else "none"
-    return {"lib_sha1": h.hexdigest(), "arch": arch,
-            "num_schedules": [lib().pld_conv_num_schedules(m) for m in sorted(MATH.values())]}
 
 
-def load_tile_cache(path):
-    """Merge schedules tuned by an earlier run (JSON written by save_tile_cache). Returns the
-    number of entries taken: 0 when the file was written by another library build or for
-    another GPU arch, and entries whose index is out of range are dropped."""
+def schedule_desc(math, idx):
+    """Stable name of schedule `idx` (pld_conv_schedule_desc); "default" for -1 (the cost
+    model's / a direct kernel's own choice)."""
+    if idx < 0:
+        return "default"
+    d = lib().pld_conv_schedule_desc(math, idx)
+    return None if d is None else d.decode()
+
+
+def _schedule_index(math, desc):
+    if desc == "default":
+        return -1
+    for i in range(lib().pld_conv_num_schedules(math)):
+        if lib().pld_conv_schedule_desc(math, i).decode() == desc:
+            return i
+    return None
+
+
+def load_tile_cache(path, arch=None):
+    """Merge a schedule table written by save_tile_cache. Entries are keyed by conv shape and
+    name their schedule by pld_conv_schedule_desc, so a table stays valid across library
+    builds; entries whose schedule this build no longer has are dropped. Returns the number of
+    entries taken (0 when the table was tuned on another GPU arch)."""
     import json
     with open(path) as f:
         d = json.load(f)
-    if not isinstance(d, dict) or d.get("meta") != _tile_cache_meta():
+    if not isinstance(d, dict) or d.get("format") != SCHEDULE_FORMAT:
         return 0
-    n_sched = dict(zip(sorted(MATH.values()), d["meta"]["num_schedules"]))
+    if d.get("arch") != (arch or _arch()):
+        return 0
     taken = 0
-    for k, v in d.get("entries", []):
-        k, v = tuple(k), int(v)
-        if -1 <= v < n_sched.get(k[-1], 0):
-            _TILE_CACHE[k] = v
+    for k, desc in d.get("entries", []):
+        k = tuple(k)
+        idx = _schedule_index(k[-1], desc)
+        if idx is not None:
+            _TILE_CACHE[k] = idx
             taken += 1
     return taken
 
 
 def save_tile_cache(path):
     import json
+    entries = sorted([list(k), schedule_desc(k[-1], v)] for k, v in _TILE_CACHE.items())
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     with open(path, "w") as f:
-        json.dump({"meta": _tile_cache_meta(),
-                   "entries": [[list(k), v] for k, v in _TILE_CACHE.items()]}, f)
+        json.dump({"format": SCHEDULE_FORMAT, "arch": _arch(),
+                   "key": ["mode", "n", "h", "w", "c1", "c2", "kh", "kw", "sh", "sw", "pad_t",
+                           "pad_l", "oh", "ow", "cout", "in_prologue", "math"],
+                   "entries": entries}, f, indent=0)
+
+
+def use_schedule_table(path=None):
+    """Fix every conv schedule from a persisted table (default: DEFAULT_SCHEDULES) and turn
+    timing-based tuning off: shapes the table does not hold run the cost model's choice.
+    Returns (entries taken, sha1 of the file)."""
+    import hashlib
+    global AUTOTUNE
+    path = path or DEFAULT_SCHEDULES
+    with open(path, "rb") as f:
+        sha = hashlib.sha1(f.read()).hexdigest()
+    _TILE_CACHE.clear()
+    n = load_tile_cache(path)
+    AUTOTUNE = False
+    return n, sha
 
 
 def _shape_key(mode, a):
@@ -357,6 +396,9 @@ def _tune(mode, a, run):
         return -1
     st = torch.cuda.current_stream()
     scheds = _schedules(mode, a.math, a)
+    # time in isolation: work queued on the engine's side streams (weight gradients, overlapped
+    # branches) must not share the GPU with the candidates
+    torch.cuda.synchronize()
     for t in scheds:
         run(t)  # warm-up (also sizes the workspace)
     # two timed passes over all candidates, best of the two per candidate: one noisy sample

@@ -28,11 +28,6 @@ from .engine_common import FlatStore, _BN, _Conv  # noqa: F401  (re-exported)
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.99
-# the expand BN's backward reductions in the depthwise dgrad's epilogue
-# (pld_dwconv_dgrad_bn_bwd) instead of a separate pass over (expand_pre, d act): measured no
-# faster at 448^2 batch 32 (1893 vs 1886 img/s, A/B on one box: the fused epilogue's extra
-# loads and swish' cost what the saved pass did), so off by default; PLD_DW_BNB=1 turns it on
-DW_BNB = os.environ.get("PLD_DW_BNB", "0") == "1"
 # keras.applications.efficientnet DEFAULT_BLOCKS_ARGS (B0): kernel, repeats, in, out, expand, stride
 B0_BLOCKS = [
     (3, 1, 32, 16, 1, 1),
@@ -101,6 +96,8 @@ class EffNetFF:
         H, W, C = input_shape
         # conv arithmetic per part (kernels.conv_policy): encoder / decoder
         self.enc_math, self.dec_math = K.conv_policy(conv_math)
+        # per decoder conv index: an arithmetic other than dec_math (precision experiments)
+        self.dec_math_override = {}
         assert C == 3 and H % 32 == 0 and W % 32 == 0, "input must be RGB with H, W % 32 == 0"
         self.H, self.W, self.B = H, W, batch_size
         self.device = torch.device(device)
@@ -115,16 +112,6 @@ class EffNetFF:
             m.bind(self)
         self.norm_scale = torch.empty(3, device=self.device)
         self.norm_shift = torch.empty(3, device=self.device)
-        # PLD_STEM_PAD (A/B, default 0): 4 widens the normalised 3-channel input with zero
-        # channels so the stem conv runs on the vectorised exact-fp32 im2col path (+0.55 % img/s,
-        # profiles/r03_stem_se_ab.txt), but its MFMA k-pairing differs from the 3-channel
-        # path's and, amplified by training-mode BN over 8 values per channel, moves the 64x64
-        # batch-2 top_activation past the 1e-3 test bar (1.13e-3); 0 keeps the scalar path with
-        # the normalisation as its input prologue. The stem stays exact fp32 either way (bf16x3:
-        # 3.8e-3 on the 448x448 prediction at batch 2)
-        self.stem_pad = int(os.environ.get("PLD_STEM_PAD", "0"))
-        if self.stem_pad:
-            self.stem.pad_input_channels(self.stem_pad)
         self.init_weights(seed)
         # thin-N 1x1 convs with the neighbouring BN (+ act, SE gate) folded in (pgemm.hip)
         self.fuse_pgemm = True
@@ -270,8 +257,6 @@ class EffNetFF:
                 self.gact[name] = torch.empty(shape, device=dev)
 
         new("input", (B, H, W, 3), grad=False)
-        if self.stem_pad:
-            new("input_pad", (B, H, W, self.stem_pad), grad=False)
         h, w = H // 2, W // 2
         new("stem_pre", (B, h, w, 32), grad=False)
         new("stem_activation", (B, h, w, 32))
@@ -365,18 +350,9 @@ class EffNetFF:
         x = A["input"]
         h, w = self.H // 2, self.W // 2
         rows = B * h * w
-        if self.stem_pad:
-            # the normalised input widened with zero channels: 16-byte rows for the vector path
-            xp = K.channel_pad_affine(x, self.stem_pad, A["input_pad"], self.norm_scale,
-                                      self.norm_shift)
-            args = a(xp, None, 3, 3, 2, pt, pl, h, w, 32, math="fp32")
-            self._conv_bn(args, self.stem.w_pad, None, A["stem_pre"], self.stem_bn, rows,
-                          training)
-        else:
-            args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift,
-                     "none", math=self._em(h, w))
-            self._conv_bn(args, self.stem.w_nat, None, A["stem_pre"], self.stem_bn, rows,
-                          training)
+        args = a(x, None, 3, 3, 2, pt, pl, h, w, 32, self.norm_scale, self.norm_shift, "none",
+                 math=self._em(h, w))
+        self._conv_bn(args, self.stem.w_nat, None, A["stem_pre"], self.stem_bn, rows, training)
         if training:
             # stem BN + swish applied by block1a's depthwise conv as it reads its taps: the stem
             # activation (its only consumer in training) is never materialised
@@ -395,7 +371,8 @@ class EffNetFF:
         for i, (conv, bn, skip) in enumerate(self.dec):
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
-            args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
+            args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout,
+                     math=self.dec_math_override.get(i, self.dec_math))
             rows = B * h * w
             bn.conv_fwd_stats(args, conv.w_nat, conv.b, A[f"dec{i}_pre"], rows, training)
             if training and i == len(self.dec) - 1 and self.fuse_final:
@@ -529,20 +506,14 @@ class EffNetFF:
         """Offset of a trainable tensor in the flat params / grads buffers."""
         return next(off for n, _, off in self.params.specs if n == name)
 
-    def backward(self, dpred, grad_ready=None):
-        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params).
-        grad_ready(offset), if given, is called (in stream order) as soon as every gradient at
-        flat offsets >= offset is final AND the parameters there are no longer read by the rest
-        of the backward (after each decoder layer's dgrad), so a data-parallel caller can reduce
-        and apply those while the rest of the backward runs (the decoder holds 99.6 % of
-        the gradient bytes, the encoder's BN parameters the rest)."""
+    def backward(self, dpred):
+        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params)."""
         A, G, B = self.act, self.gact, self.B
         a = K.conv_args
         h, w = self.H, self.W
-        ready = grad_ready or (lambda off: None)
         # the side stream needs its own buffers: gradients it reads are never recycled by the
         # main stream's later layers (slot "dec"), its bias sums use their own workspace
-        side = bool(self.overlap_wgrad) and grad_ready is None
+        side = bool(self.overlap_wgrad)
         main = torch.cuda.current_stream(self.device)
         if side:
             wstream, fork = self._wgrad_side()
@@ -569,7 +540,6 @@ class EffNetFF:
             K.conv2d_dgrad(args, dpred, self.final.w_dg, G["dec4_up"])
         # after the layer's dgrad: its filter copies are no longer read this step (a caller
         # may update and refresh them from here on)
-        ready(self.param_offset("dec_conv5/kernel"))
         for i in range(len(self.dec) - 1, -1, -1):
             conv, bn, skip = self.dec[i]
             h, w = h // 2, w // 2
@@ -588,7 +558,8 @@ class EffNetFF:
                 g1, g2 = G[f"dec{i - 1}_up"], (G[pskip] if pskip else None)
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
-            args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout, math=self.dec_math)
+            args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout,
+                     math=self.dec_math_override.get(i, self.dec_math))
             if side:
                 def wg(args=args, gpre=gpre, rows=rows, conv=conv):
                     K.conv2d_wgrad(args, gpre, conv.dw)
@@ -604,7 +575,6 @@ class EffNetFF:
                 K.conv2d_wgrad(args, gpre, conv.dw)
                 K.channel_sum(gpre, rows, conv.cout, conv.db)
             K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
-            ready(self.param_offset(f"dec_conv{i}/kernel"))
         if side and deferred:
             fork[-1].record(main)
             with torch.cuda.stream(wstream):
@@ -628,7 +598,6 @@ class EffNetFF:
         self.stem_bn.bwd(A["stem_pre"], G["stem_activation"], rows, "swish", None)
         if side:  # join: every weight gradient is final on the caller's stream from here
             main.wait_stream(wstream)
-        ready(0)
 
     def _block_bwd(self, blk, x_in, gx_in):
         A, G, B, n = self.act, self.gact, self.B, blk["name"]
@@ -666,39 +635,17 @@ class EffNetFF:
             ebn = blk["expand_bn"]
             bnp = (ebn.mean, ebn.invstd, ebn.gamma, ebn.beta)
             k12 = self._k12_buf(blk["cexp"])
-            if not DW_BNB:  # A/B knob: the unfused sequence (dgrad, then the BN backward)
-                K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
-                               accumulate=is_tap)
-                if blk["fused_expand_dgrad"]:
-                    K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp,
-                                    "swish", ebn.dgamma, ebn.dbeta, k12)
-                    K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp,
-                                   "swish", k12, blk["expand"].w_dg, blk["cin"], gx_in)
-                else:
-                    gpe = self._gpre_buf(A[n + "expand_pre"].shape)
-                    ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
-                    K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                               math=self._em(h, w)), gpe,
-                                   blk["expand"].w_dg, gx_in)
-            elif blk["fused_expand_dgrad"]:
-                # the depthwise dgrad gathers the expand BN's backward reductions as it stores
-                # d(expand activation) (no separate pass over (expand_pre, ge)); the expand
-                # conv's input gradient then reads (expand_pre, ge) through the BN backward
-                # (pgemm): the BN's dx is never materialised
-                K.dwconv_dgrad_bn_bwd(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
-                                      A[n + "expand_pre"], bnp, "swish", ebn.dgamma, ebn.dbeta,
-                                      k12, accumulate=is_tap)
-                K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], ebn.mean,
-                               ebn.invstd, ebn.gamma, ebn.beta, "swish", k12,
-                               blk["expand"].w_dg, blk["cin"], gx_in)
+            K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
+            if blk["fused_expand_dgrad"]:
+                K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp, "swish",
+                                ebn.dgamma, ebn.dbeta, k12)
+                K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp, "swish",
+                               k12, blk["expand"].w_dg, blk["cin"], gx_in)
             else:
                 gpe = self._gpre_buf(A[n + "expand_pre"].shape)
-                K.dwconv_dgrad_bn_bwd(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge,
-                                      A[n + "expand_pre"], bnp, "swish", ebn.dgamma, ebn.dbeta,
-                                      k12, dx=gpe, accumulate=is_tap)
+                ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
                 K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                           math=self._em(h, w)), gpe,
-                               blk["expand"].w_dg, gx_in)
+                                           math=self._em(h, w)), gpe, blk["expand"].w_dg, gx_in)
         else:
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)
         if blk["residual"]:

@@ -71,9 +71,6 @@ class _BN:
         self.invstd = torch.empty(self.c, device=dev)
         self.inf_scale = torch.empty(self.c, device=dev)
         self.inf_shift = torch.empty(self.c, device=dev)
-        # training-mode affine form (train_coeffs): the consuming conv's input prologue
-        self.scale = torch.empty(self.c, device=dev)
-        self.shift = torch.empty(self.c, device=dev)
 
     def stats_(self, x, rows, training):
         if training:
@@ -92,12 +89,6 @@ class _BN:
         else:
             K.conv2d_fwd(args, w_nat, bias, y)
             self.stats_(y, rows, False)
-
-    def train_coeffs(self):
-        """scale = gamma*invstd, shift = beta - mean*scale from this step's batch statistics:
-        a conv that reads the BN input through act(x*scale + shift) (conv_args in_scale /
-        in_shift) never needs the BN output materialised."""
-        K.bn_train_coeffs(self.mean, self.invstd, self.gamma, self.beta, self.scale, self.shift)
 
     def apply(self, x, rows, act, y, training, gate=None, hw=0):
         if training:
@@ -170,21 +161,3 @@ class _Conv:
 
     def refresh(self):
         K.filter_refresh(self.w, self.w_nat, self.w_nat_x3, self.w_dg, self.w_dg_x3)
-        if getattr(self, "cpad", 0):
-            self._refresh_padded()
-
-    def pad_input_channels(self, cpad):
-        """Serve this (frozen, input-layer) conv from an input widened to `cpad` channels with
-        zeros (K.channel_pad_affine): a native filter with zero taps for the extra channels
-        (+ its bf16x3 split when cpad % 8 == 0), rebuilt by refresh()."""
-        self.cpad = cpad
-        self.w_pad = torch.empty(self.cout, self.k, self.k, cpad, device=self.w.device)
-        self.w_pad_x3 = torch.empty_like(self.w_pad) if cpad % 8 == 0 else None
-        self._refresh_padded()
-
-    def _refresh_padded(self):
-        wp = torch.zeros(self.k, self.k, self.cpad, self.cout, device=self.w.device)
-        wp[:, :, :self.cin, :] = self.w  # layout plumbing, once per weight load
-        K.filter_to_native(wp, self.w_pad)
-        if self.w_pad_x3 is not None:
-            K.filter_split(self.w_pad, self.w_pad_x3)

@@ -44,7 +44,7 @@ TAPS = ("conv2_block3_out", "conv3_block4_out", "conv4_block3_out", "conv5_block
 # Only the FORWARD convs of those stages need it: the activations' rounding is what the chaotic
 # encoder amplifies; the backward's dX convs of the frozen encoder run bf16x3 (their ~2^-16
 # per-product error sits far below the fp32 restatement's own gradient error, ~5e-2 per tensor
-# at batch 32; PLD_REDWEB_EXACT_BWD=1 keeps the backward exact too, for A/B).
+# at batch 32).
 EXACT_STAGES_AUTO = ("conv2",)
 FFLS = [("ffl0", 256, 256, "conv4_block3_out"),
         ("ffl1", 128, 128, "conv3_block4_out"),
@@ -78,26 +78,11 @@ class RedWebFF:
         self.stats.materialize(self.device)
         for m in self.bns + self.convs:
             m.bind(self)
-        # PLD_STEM_PAD (A/B, default 0): the 3-channel input widened to 8 channels (zeros) so the
-        # 7x7 stem runs on the bf16x3 im2col kernel: measured 866 -> 861 img/s (2.7x the FLOPs
-        # of the zero channels; profiles/r03_stem_se_ab.txt), so the scalar exact path stays
-        self.stem_pad = int(os.environ.get("PLD_STEM_PAD", "0"))
-        if self.stem_pad:
-            self.stem.pad_input_channels(self.stem_pad)
         self.init_weights(seed)
         self._alloc()
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
-        self.exact_bwd = os.environ.get("PLD_REDWEB_EXACT_BWD", "0") == "1"
-        # PLD_BN_PROLOGUE (A/B, default 0): encoder bottlenecks in training read conv1 / conv2's
-        # pre-BN output through the BN + ReLU input prologue of the next conv (1 = conv2 and
-        # conv3, 2 = conv3 only, 3 = conv2 only), so those BN outputs are never materialised.
-        # Measured on MI355X (profiles/r03_prologue_ab.txt): it removes 0.5 ms of bn_apply per
-        # step but the prologue'd bf16x3 convs run 0.9 ms slower (the conv kernel is issue- and
-        # latency-bound: ~30 % per launch for 2 loads + 8 FMAs per staged float4), 873 -> 863
-        # img/s; so the BN outputs stay materialised.
-        self.bn_prologue = int(os.environ.get("PLD_BN_PROLOGUE", "0"))
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
         self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
         # forward: each feature-fusion layer's left branch (conv0 + bn0 + block_left: it reads
@@ -215,8 +200,6 @@ class RedWebFF:
                 self.gact[name] = torch.empty(shape, device=dev)
 
         new("input", (B, H, W, 3), grad=False)
-        if self.stem_pad:
-            new("input_pad", (B, H, W, self.stem_pad), grad=False)
         h, w = H // 2, W // 2
         new("conv1_pre", (B, h, w, 64), grad=False)
         new("conv1_relu", (B, h, w, 64))
@@ -277,29 +260,22 @@ class RedWebFF:
     def _math(self, conv, oh=None, ow=None, bwd=False):
         if conv.trainable:
             return self.dec_math
-        if (self.enc_math == "auto" and conv.name.startswith(self.exact_stages)
-                and (not bwd or self.exact_bwd)):
+        if self.enc_math == "auto" and conv.name.startswith(self.exact_stages) and not bwd:
             return "fp32"
         # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
         return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
                               getattr(self, "x3_min_population", None))
 
-    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None, bn=None, training=True,
-              pro=None):
+    def _conv(self, conv, x, y, h, w, oh, ow, acc=False, x2=None, bn=None, training=True):
         """'same' (stride 1) or unpadded strided conv of x [B,h,w,cin] into y [B,oh,ow,cout];
-        with `bn`, also that BN's statistics of y (fused into the conv epilogue in training);
-        with `pro` (a BN whose train_coeffs are current), the conv reads relu(pro(x))."""
+        with `bn`, also that BN's statistics of y (fused into the conv epilogue in training)."""
         k, s = conv.k, conv.stride
         if s == 1:
             pt, pl = (k - 1) // 2, (k - 1) // 2
         else:
             pt = pl = 0
-        if pro is not None:
-            args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout, pro.scale, pro.shift,
-                               "relu", math=self._math(conv, oh, ow))
-        else:
-            args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
-                               math=self._math(conv, oh, ow))
+        args = K.conv_args(x, x2, k, k, s, pt, pl, oh, ow, conv.cout,
+                           math=self._math(conv, oh, ow))
         if bn is not None:
             assert not acc and x2 is None
             bn.conv_fwd_stats(args, conv.w_nat, conv.b, y, self.B * oh * ow, training)
@@ -313,8 +289,6 @@ class RedWebFF:
         h, w = H // 2, W // 2
         # stem: ZeroPadding2D(3) + 7x7/2 valid conv (+bias), BN, ReLU, ZeroPadding2D(1) + pool
         x0, w0 = A["input"], self.stem.w_nat
-        if self.stem_pad:  # the 3-channel input widened with zeros (EffNetFF.stem_pad)
-            x0, w0 = K.channel_pad_affine(A["input"], self.stem_pad, A["input_pad"]), self.stem.w_pad
         args = K.conv_args(x0, None, 7, 7, 2, 3, 3, h, w, 64, math=self._math(self.stem, h, w))
         self.stem_bn.conv_fwd_stats(args, w0, self.stem.b, A["conv1_pre"], B * h * w, training)
         self.stem_bn.apply(A["conv1_pre"], B * h * w, "relu", A["conv1_relu"], training)
@@ -365,32 +339,12 @@ class RedWebFF:
         else:
             sc = x
         self._conv(blk["c1"], x, A[n + "1_pre"], h, w, oh, ow, bn=blk["bn1"], training=training)
-        if training and self.bn_prologue:
-            # conv2 reads 1_pre through bn1 + ReLU; conv3 reads 2_pre through bn2 + ReLU unless
-            # its 1x1 GEMM runs on the streaming wide kernel (no prologue there): then 2_relu
-            if self.bn_prologue in (1, 3):
-                blk["bn1"].train_coeffs()
-                self._conv(blk["c2"], A[n + "1_pre"], A[n + "2_pre"], oh, ow, oh, ow,
-                           bn=blk["bn2"], training=training, pro=blk["bn1"])
-            else:
-                blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
-                self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
-                           bn=blk["bn2"], training=training)
-            if self.bn_prologue == 3 or self._wide(blk["c3"], A[n + "2_pre"], oh, ow):
-                blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
-                self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
-                           bn=blk["bn3"], training=training)
-            else:
-                blk["bn2"].train_coeffs()
-                self._conv(blk["c3"], A[n + "2_pre"], A[n + "3_pre"], oh, ow, oh, ow,
-                           bn=blk["bn3"], training=training, pro=blk["bn2"])
-        else:
-            blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
-            self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow,
-                       bn=blk["bn2"], training=training)
-            blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
-            self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow,
-                       bn=blk["bn3"], training=training)
+        blk["bn1"].apply(A[n + "1_pre"], rows, "relu", A[n + "1_relu"], training)
+        self._conv(blk["c2"], A[n + "1_relu"], A[n + "2_pre"], oh, ow, oh, ow, bn=blk["bn2"],
+                   training=training)
+        blk["bn2"].apply(A[n + "2_pre"], rows, "relu", A[n + "2_relu"], training)
+        self._conv(blk["c3"], A[n + "2_relu"], A[n + "3_pre"], oh, ow, oh, ow, bn=blk["bn3"],
+                   training=training)
         if join is not None:
             torch.cuda.current_stream(self.device).wait_event(join)
         blk["bn3"].add_apply(A[n + "3_pre"], rows, sc, "relu", A[n + "out"], training)
@@ -403,13 +357,6 @@ class RedWebFF:
             self._pside = (torch.cuda.Stream(device=self.device), torch.cuda.Event(),
                            torch.cuda.Event())
         return self._pside
-
-    def _wide(self, conv, x, h, w):
-        """Whether this stride-1 1x1 conv's forward runs on the streaming wide / thin kernels
-        (which take no input prologue)."""
-        args = K.conv_args(x, None, conv.k, conv.k, 1, 0, 0, h, w, conv.cout,
-                           math=self._math(conv, h, w))
-        return K.conv_kernel_name(args, "fwd") in ("wide1x1_kernel", "thin1x1_kernel")
 
     def _bottleneck_fwd(self, bt, x, h, w, training):
         A, n = self.act, bt["name"]
@@ -521,14 +468,11 @@ class RedWebFF:
         """Offset of a trainable tensor in the flat params / grads buffers."""
         return next(off for n, _, off in self.params.specs if n == name)
 
-    def backward(self, dpred, grad_ready=None):
-        """grad_ready(offset): as EffNetFF.backward — called once the decoder's gradients (the
-        tail of the flat buffer, from its first trainable conv on) are final, and at the end."""
+    def backward(self, dpred):
+        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params)."""
         A, G, B = self.act, self.gact, self.B
-        ready = grad_ready or (lambda off: None)
-        # decoder weight gradients on a side stream (EffNetFF.backward); a data-parallel caller
-        # (grad_ready) keeps the single-stream order
-        self._side = bool(self.overlap_wgrad) and grad_ready is None
+        # decoder weight gradients on a side stream (EffNetFF.backward)
+        self._side = bool(self.overlap_wgrad)
         self._deferred = []
         main = torch.cuda.current_stream(self.device)
         H, W = self.H, self.W
@@ -561,8 +505,6 @@ class RedWebFF:
                 for wg in self._deferred:
                     wg()
         self._deferred = []
-        ready(min(off for n, _, off in self.params.specs
-                  if any(c.trainable and n == c.wk for c in self.convs)))
         K.upsample2x_bwd(G["conv5_up"], G["conv5_block3_out"])
         # encoder (taps already hold their decoder gradient: accumulate onto them)
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -582,7 +524,6 @@ class RedWebFF:
         if self._side:  # join: every weight gradient is final on the caller's stream
             main.wait_stream(self._wgrad_side()[0])
         self._side = False
-        ready(0)
 
     def _block_bwd(self, blk, x, gx, gx_is_tap):
         A, G, B, n = self.act, self.gact, self.B, blk["name"]

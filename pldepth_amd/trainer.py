@@ -78,9 +78,7 @@ class ReplicaTrainer:
         self.lr_dev = torch.full((1,), 0.01, device=dev)
         self.m, self.v, self.vhat = self.engine.adam_state()
         self.graphs = None
-        # PLD_STREAM_PRIO=1: the step's stream at high priority (side streams stay default)
-        prio = -1 if os.environ.get("PLD_STREAM_PRIO", "0") == "1" else 0
-        self.stream = torch.cuda.Stream(device=dev, priority=prio)
+        self.stream = torch.cuda.Stream(device=dev)
         self.side = torch.cuda.Stream(device=dev)  # per-bucket optimizer updates (N > 1)
 
     # ------------------------------------------------------------------ data

@@ -41,3 +41,19 @@ def fixed_schedules():
     K.AUTOTUNE = saved[0]
     K._TILE_CACHE.clear()
     K._TILE_CACHE.update(saved[1])
+
+
+@pytest.fixture
+def bench_schedules():
+    """The bench's persisted conv schedule table (kernels.DEFAULT_SCHEDULES, written by
+    `bench.py --tune`) with timing-based tuning off: a test using it runs exactly the schedules
+    bench.py's timed steps run (bench.py loads the same table by default). Yields the table's
+    sha1; restores the previous tuning state afterwards."""
+    from pldepth_amd import kernels as K
+    saved = (K.AUTOTUNE, dict(K._TILE_CACHE))
+    n, sha = K.use_schedule_table()
+    assert n > 0, "the schedule table holds no entry for this GPU arch"
+    yield sha
+    K.AUTOTUNE = saved[0]
+    K._TILE_CACHE.clear()
+    K._TILE_CACHE.update(saved[1])

@@ -57,3 +57,56 @@ def test_header_documents_reference_replacements():
     for ref in ["depth_utils.py:39-61", "nll_loss.py", "PLDepth.py:133", "pl_hourglass.py",
                 "sampling.py"]:
         assert ref in txt, ref
+
+
+def test_schedule_names_are_unique_and_resolve():
+    """pld_conv_schedule_desc names every schedule once per math; the persisted table
+    (kernels.DEFAULT_SCHEDULES) names only schedules this build has, for gfx950."""
+    import json
+
+    from pldepth_amd import kernels as K
+    lib = _lib.lib()
+    for math in K.MATH.values():
+        n = lib.pld_conv_num_schedules(math)
+        names = [lib.pld_conv_schedule_desc(math, i).decode() for i in range(n)]
+        assert len(set(names)) == n, names
+        assert lib.pld_conv_schedule_desc(math, n) is None
+        assert all(K._schedule_index(math, d) == i for i, d in enumerate(names))
+    if os.path.exists(K.DEFAULT_SCHEDULES):
+        d = json.load(open(K.DEFAULT_SCHEDULES))
+        assert d["format"] == K.SCHEDULE_FORMAT and d["arch"].startswith("gfx950")
+        assert d["entries"]
+        for key, desc in d["entries"]:
+            assert len(key) == len(d["key"])
+            assert K._schedule_index(key[-1], desc) is not None, (key, desc)
+        # the same entries are taken on a gfx950 device (arch given: no GPU here)
+        saved = dict(K._TILE_CACHE)
+        try:
+            K._TILE_CACHE.clear()
+            assert K.load_tile_cache(K.DEFAULT_SCHEDULES, arch=d["arch"]) == len(d["entries"])
+        finally:
+            K._TILE_CACHE.clear()
+            K._TILE_CACHE.update(saved)
+
+
+def test_bench_self_spawn_command(monkeypatch):
+    """bench.py --gpus N without a launcher runs torch.distributed.run with N ranks on
+    127.0.0.1 as one child process and exits with its code (no GPU call in the parent)."""
+    import subprocess as sp
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(sp, "call", fake_call)
+    assert bench.spawn_ranks(8, ["--gpus", "8", "--steps", "3"]) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")

@@ -40,5 +40,26 @@ def test_bench_world2_gloo_line(cuda):
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
     assert out["config"]["parallelism"] == "dp2" and out["config"]["backend"] == "gloo"
     assert out["config"]["graph"] is True
+    assert out["config"]["ranks_seen"] == 2
     assert out["value"] > 0 and out["steps"] == 3
     assert out["loss"] == out["loss"]  # finite
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_spawns_ranks(cuda):
+    """`python bench.py --gpus 2` with no launcher (no WORLD_SIZE), as the driver invokes the
+    N = 1 bench: bench.py starts the two ranks itself and rank 0 prints the one line."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "2", "--backend", "gloo", "--size", "224", "--batch", "8",
+           "--no-extra-configs", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["ranks_seen"] == 2
+    assert out["config"]["backend"] == "gloo" and out["config"]["global_batch"] == 16
+    assert out["value"] > 0

@@ -12,11 +12,10 @@
 * cfg5: the full-size ListMLE (B=32, R=1000, L=64: 2,048,000 list elements, heavy duplicate
   pixels) against oracle/listmle.py.
 
-Gradient bar (BASELINE.json: 1e-3 relative): per tensor max(1e-3, 4x the fp32 restatement's own
-error) — wherever the fp32 restatement of the reference semantics lands within 2.5e-4 of fp64,
-the HIP gradient must be within 1e-3 — and over all tensors together a global rel-L2 within
-max(1e-3, 2x the fp32 restatement's). The gradients of the reference semantics are themselves
-ill-conditioned at the 1e-3 level: training-mode BN cancels most of each incoming gradient, and
+Gradient bar (BASELINE.json: 1e-3 relative): per tensor 1e-3 wherever the fp32 restatement of
+the reference semantics itself lands within 1e-3 of fp64, else 4x the fp32 restatement's own
+error; over all tensors together a global rel-L2 within max(1e-3, 2x the fp32 restatement's).
+The gradients of the reference semantics are themselves ill-conditioned at the 1e-3 level: training-mode BN cancels most of each incoming gradient, and
 an exact fp32 implementation lands ~1 % (median per tensor) from fp64 at batch 2 AND at the
 bench's batch 32 (ff_effnet 5 of 98 tensors within 1e-3, ff_redweb 3 of 237; profiles/r03_parity).
 bf16x3 products carry ~2^8 the rounding of fp32 ones; measured HIP / fp32-restatement error
@@ -84,7 +83,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero):
     rows, fails = {}, []
     for k in keys:
         e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64[k])
-        bar = max(TOL, 4.0 * e32)
+        bar = TOL if e32 <= TOL else 4.0 * e32
         rows[k] = {"hip": e_hip, "fp32_restatement": e32, "bar": bar}
         if e_hip > bar:
             fails.append((k, e_hip, e32))
@@ -383,11 +382,12 @@ def _oracle_step(O, P, x, y, B, L, taps=None, **kw):
 
 @pytest.mark.timeout(1500)
 @pytest.mark.parametrize("model", ["ff_effnet", "ff_redweb"])
-def test_batch32_bench_policy(cuda, model):
+def test_batch32_bench_policy(cuda, model, bench_schedules):
     """cfg2 / cfg3 exactly as the bench runs them: 448x448, batch 32, the default 'auto' conv
     policy (ff_effnet: bf16x3 everywhere; ff_redweb: bf16x3 except the stem and conv2 stage,
-    RedWebFF.exact_stages). Forward taps, prediction, loss and every trainable gradient against
-    the fp64 oracle, next to the torch-CPU fp32 restatement of the same reference semantics on
+    RedWebFF.exact_stages) and the bench's own persisted conv schedule table
+    (kernels.DEFAULT_SCHEDULES, the bench_schedules fixture). Forward taps, prediction, loss
+    and every trainable gradient against the fp64 oracle, next to the torch-CPU fp32 restatement of the same reference semantics on
     the same input: every tap and the prediction within max(1e-3, 2x the fp32 restatement's
     error), the loss within 1e-3, the gradients by check_gradients' bar (1e-3 wherever the
     fp32 restatement meets it). Reports go to $PLD_REPORT_DIR."""
@@ -444,11 +444,8 @@ def test_batch32_bench_policy(cuda, model):
     errs["loss"] = abs(hip_loss - loss_ref) / abs(loss_ref)
     bars = {n: max(TOL, 2.0 * e32[n]) for n in e32}
     bars["loss"] = TOL
-    report(f"{model}_b32_auto_forward", {"errors": errs, "bars": bars, "fp32_restatement": e32})
+    report(f"{model}_b32_auto_forward", {"errors": errs, "bars": bars, "fp32_restatement": e32,
+                                         "schedule_table_sha1": bench_schedules})
     print(errs, bars)
     assert all(errs[n] < bars[n] for n in errs), (errs, bars)
-    glob = check_gradients(f"{model}_b32_auto_grads", hip_grads, g64, g32, zero)
-    # HIP is as close to fp64 as an exact fp32 implementation of the reference semantics: no
-    # more tensors outside 1e-3 than the fp32 restatement has, give or take 10 % of them
-    assert glob["tensors_hip_within_1e-3"] >= glob["tensors_fp32_within_1e-3"] - \
-        max(1, glob["tensors"] // 10), glob
+    check_gradients(f"{model}_b32_auto_grads", hip_grads, g64, g32, zero)
