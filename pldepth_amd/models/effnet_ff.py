@@ -96,8 +96,9 @@ class EffNetFF:
         H, W, C = input_shape
         # conv arithmetic per part (kernels.conv_policy): encoder / decoder
         self.enc_math, self.dec_math = K.conv_policy(conv_math)
-        # per decoder conv index: an arithmetic other than dec_math (precision experiments)
-        self.dec_math_override = {}
+        # per decoder conv index: an arithmetic other than dec_math for its forward / its
+        # backward (precision experiments, tools/exp_dec_precision.py)
+        self.dec_math_fwd, self.dec_math_bwd = {}, {}
         assert C == 3 and H % 32 == 0 and W % 32 == 0, "input must be RGB with H, W % 32 == 0"
         self.H, self.W, self.B = H, W, batch_size
         self.device = torch.device(device)
@@ -372,7 +373,7 @@ class EffNetFF:
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
             args = a(x, x2, 3, 3, 1, pt, pl, h, w, conv.cout,
-                     math=self.dec_math_override.get(i, self.dec_math))
+                     math=self.dec_math_fwd.get(i, self.dec_math))
             rows = B * h * w
             bn.conv_fwd_stats(args, conv.w_nat, conv.b, A[f"dec{i}_pre"], rows, training)
             if training and i == len(self.dec) - 1 and self.fuse_final:
@@ -559,7 +560,7 @@ class EffNetFF:
             pt, _ = same_pad(h, 3, 1)
             pl, _ = same_pad(w, 3, 1)
             args = a(x1, x2, 3, 3, 1, pt, pl, h, w, conv.cout,
-                     math=self.dec_math_override.get(i, self.dec_math))
+                     math=self.dec_math_bwd.get(i, self.dec_math))
             if side:
                 def wg(args=args, gpre=gpre, rows=rows, conv=conv):
                     K.conv2d_wgrad(args, gpre, conv.dw)

@@ -44,7 +44,16 @@ def timed_step(tr, lr):
                 M, N, Kd = args.n * args.h * args.w, args.c1 + args.c2, args.kh * args.kw * args.cout
             else:
                 M, N, Kd = args.kh * args.kw * (args.c1 + args.c2), args.cout, args.n * args.oh * args.ow
-            recs.append((mode, M, N, Kd, args.kh, args.tile, e0, e1))
+            saved = args.tile
+            args.tile = getattr(args, "_used_tile", saved)
+            kname = K.conv_kernel_name(args, mode.split("+")[0] if mode != "fwd_bn_stats"
+                                       else "fwd")
+            sched = K.schedule_desc(args.math, args.tile)
+            args.tile = saved
+            by = 4.0 * (args.n * args.h * args.w * (args.c1 + args.c2)
+                        + args.n * args.oh * args.ow * args.cout
+                        + args.kh * args.kw * (args.c1 + args.c2) * args.cout)
+            recs.append((mode, M, N, Kd, args.kh, (kname, sched, by), e0, e1))
             return r
         return w
 
@@ -69,11 +78,15 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--math", nargs="+", default=["auto", "mixed", "fp32"])
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--schedules", default="",
+                    help="persisted schedule table (kernels.use_schedule_table): no tuning")
     a = ap.parse_args()
     import bench
     from pldepth_amd import kernels as K
     from pldepth_amd.trainer import ReplicaTrainer
     torch.cuda.set_device(0)
+    if a.schedules:
+        print("schedule table entries:", K.use_schedule_table(a.schedules)[0])
     H = a.size
     tr = ReplicaTrainer((H, H, 3), a.batch, 5, 100, 1, seed=0, model=a.model)
     x, gt, mask = bench.synthetic_batch(a.batch, H, H, seed=1000)
@@ -90,13 +103,14 @@ def main():
     base = tables[a.math[0]]
     order = sorted(range(len(base)), key=lambda i: -base[i][6])
     hdr = "  ".join(f"{m:>16}" for m in a.math)
-    print(f"{'mode':6} {'M':>9} {'N':>5} {'K':>8} k  {hdr}")
+    print(f"{'mode':6} {'M':>9} {'N':>5} {'K':>8} k  {hdr}   kernel / schedule / GB/s")
     for i in order[:a.top]:
-        mode, M, N, Kd, k, _, _ = base[i]
+        mode, M, N, Kd, k, (kname, sched, by), _ = base[i]
         fl = 2.0 * M * N * Kd
         cells = "  ".join(f"{tables[m][i][6]:7.3f}ms {fl / tables[m][i][6] / 1e9:5.0f}TF"
                           for m in a.math)
-        print(f"{mode:6} {M:9d} {N:5d} {Kd:8d} {k}  {cells}")
+        print(f"{mode:6} {M:9d} {N:5d} {Kd:8d} {k}  {cells}   {kname} {sched} "
+              f"{by / base[i][6] / 1e6:6.0f}")
     for m in a.math:
         tot = sum(r[6] for r in tables[m])
         fl = sum(2.0 * r[1] * r[2] * r[3] for r in tables[m])

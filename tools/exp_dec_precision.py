@@ -27,7 +27,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--schedules", default="")
     ap.add_argument("--out", default="")
-    ap.add_argument("--variants", default="auto,dec_fp32,dec4_fp32,dec34_fp32,dec01_fp32,mixed,fp32")
+    ap.add_argument("--variants", 
+                    default="auto,auto2,dec_fp32,dec01_fp32,dec01_fwd,dec01_bwd,dec0_fwd,dec1_fwd,"
+                            "dec2_fwd,mixed")
     a = ap.parse_args()
     from oracle import effnet as OE
     from pldepth_amd import kernels as K
@@ -41,14 +43,22 @@ def main():
     x = rng.random((B, H, H, 3)).astype(np.float32)
     y = make_rankings(rng, B, H, H, R, L)
     res, weights = {}, None
+    print("variants: auto = the bench policy; autoN = a repeat (run-to-run spread)", flush=True)
     for var in a.variants.split(","):
-        policy = {"mixed": "mixed", "fp32": "fp32"}.get(var, "auto")
+        policy = {"mixed": "mixed", "fp32": "fp32"}.get(var.rstrip("0123456789"), "auto")
         eng = EffNetFF((H, H, 3), B, seed=0, conv_math=policy)
         eng.drop_connect = False
+        print(var, "enc", eng.enc_math, "dec", eng.dec_math, flush=True)
         if var == "dec_fp32":
             eng.dec_math = "fp32"
-        if var.startswith("dec") and var != "dec_fp32":  # e.g. dec34_fp32: decoder convs 3, 4
-            eng.dec_math_override = {int(c): "fp32" for c in var[3:var.index("_")]}
+        if var.startswith("dec") and var != "dec_fp32":
+            # decNN_fp32: decoder convs N.. fp32 forward + backward; decNN_fwd / decNN_bwd: one
+            # direction only
+            idx = {int(c): "fp32" for c in var[3:var.index("_")]}
+            if not var.endswith("_bwd"):
+                eng.dec_math_fwd = dict(idx)
+            if not var.endswith("_fwd"):
+                eng.dec_math_bwd = dict(idx)
         weights = eng.get_weights()
         eng.act["input"].copy_(torch.from_numpy(x))
         pred = eng.forward(training=True)
@@ -56,6 +66,9 @@ def main():
         eng.backward(dpred)
         torch.cuda.synchronize()
         res[var] = {k: eng.grads[k].detach().cpu().double() for k in OE.trainable_names(weights)}
+        if var == "auto":  # the BN statistics of the decoder stages (batch mean / invstd)
+            bnstat = {i: (bn.mean.double().cpu(), bn.invstd.double().cpu())
+                      for i, (_, bn, _) in enumerate(eng.dec)}
         del eng, pred, dpred
         torch.cuda.empty_cache()
         print("ran", var, flush=True)
@@ -74,6 +87,22 @@ def main():
         out[var] = {"global_rel_l2": glob, "watch": {k: e[k] for k in WATCH},
                     "within_1e-3": sum(v <= 1e-3 for v in e.values())}
         print(var, json.dumps(out[var]), flush=True)
+    # per output channel of dec_conv4/kernel: where the auto run's error sits, against the
+    # channel's BN-4 statistics (mean / std of dec4_pre) and its gradient magnitude
+    if "auto" in res:
+        k = "dec_conv4/kernel"
+        ref, hip = g64[k].double(), res["auto"][k]
+        mx = float(ref.abs().max())
+        per = ((hip - ref).abs().amax(dim=(0, 1, 2)) / mx).tolist()
+        mag = (ref.abs().amax(dim=(0, 1, 2)) / mx).tolist()
+        mean, invstd = bnstat[4]
+        print("cout  err/max|ref|  max|ref_c|/max|ref|  bn4 |mean|/std")
+        for c in sorted(range(len(per)), key=lambda c: -per[c])[:8]:
+            print(f"{c:4d}  {per[c]:.3e}  {mag[c]:.3e}  {abs(float(mean[c])) * float(invstd[c]):.2f}")
+        for i in range(4):
+            m, s_ = bnstat[i]
+            r = (m.abs() * s_)
+            print(f"bn{i}: |mean|/std max {float(r.max()):.2f} median {float(r.median()):.2f}")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
