@@ -42,7 +42,24 @@ struct GemmConvParams {
   // [N][stats_parts][2], stats_parts = M tiles x (BM / wave rows); NULL = off
   double* stats;
   int stats_parts;
+  // bf16x3 tile-stream schedule (conv_x3_kernel, sk_nk > 0): a 1-D grid of G workgroups walks
+  // the (tile, K-step) space tile-major, tile t = (mb = t / sk_nnb, nb = t % sk_nnb), sk_nk
+  // K-steps per tile. sk_align = 1: workgroup w owns whole tiles [w T/G, (w+1) T/G) (T =
+  // sk_tiles); 0: steps [w S/G, (w+1) S/G) (S = T sk_nk), a tile cut between workgroups leaves
+  // raw fp32 partial sums in sk_slab ([G][2][BM][BN]: a workgroup's first, then last tile) that
+  // pld's stream fixup kernel sums in K order and stores through the epilogue.
+  int sk_nk, sk_tiles, sk_nnb, sk_align;
+  float* sk_slab;
 };
+
+// first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)
+__host__ __device__ inline long sk_begin(const GemmConvParams& p, long w, long G) {
+  return p.sk_align ? (w * p.sk_tiles / G) * p.sk_nk : w * ((long)p.sk_tiles * p.sk_nk) / G;
+}
+// the workgroup whose range holds global step s (non-aligned schedule)
+__host__ __device__ inline long sk_owner(const GemmConvParams& p, long s, long G) {
+  return ((s + 1) * G - 1) / ((long)p.sk_tiles * p.sk_nk);
+}
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 

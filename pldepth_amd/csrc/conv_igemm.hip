@@ -816,7 +816,8 @@ extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows
 extern "C" int pld__x3_num_cfg(void);
 extern "C" int pld__x3_cfg_dims(int cfg, int* bm, int* bn, int* tm, int* tn, int* occ);
 extern "C" int pld__x3_wgrad_cfg_ok(int cfg);
-extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream);
+extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, int sk_grid,
+                              void* stream);
 extern "C" int pld__x3_num_patch(void);
 extern "C" int pld__x3_patch_bn(int cfg);
 extern "C" int pld__x3_patch_ok(const GemmConvParams* p, int cfg);
@@ -836,15 +837,19 @@ static bool x3_fwd_geom(int C, int c1, bool prologue, int taps) {
 
 // Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), [2 n3,
 // 2 n3 + np) the bf16x3 patch kernel (3x3, 32-channel inputs; other shapes take the default
-// tile), then [2 n3 + np, ... + kNumTiles) the exact-fp32 schedules — the per-shape autotuner
-// may keep fp32 where it is faster (e.g. HBM-bound K <= 32 convs); it is never less accurate.
-// Resolves (math, eligible geometry, tile) to (x3 kernel?, patch kernel?, tile in that space).
+// tile), [2 n3 + np, 3 n3 + np) the bf16x3 tiles as a tile stream (conv_x3_kernel STREAM: a
+// 1-D grid walking (tile, K-step) ranges), then the exact-fp32 schedules — the per-shape
+// autotuner may keep fp32 where it is faster (e.g. HBM-bound K <= 32 convs); it is never less
+// accurate. Resolves (math, eligible geometry, tile) to (x3 kernel?, patch kernel?, stream?,
+// tile in that space).
+static int x3_sched_count() { return 3 * pld__x3_num_cfg() + pld__x3_num_patch(); }
 static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t,
-                          bool* patch = nullptr) {
-  const int n3 = pld__x3_num_cfg(), nx = 2 * n3 + pld__x3_num_patch();
+                          bool* patch = nullptr, bool* stream = nullptr) {
+  const int n3 = pld__x3_num_cfg(), np = pld__x3_num_patch(), nx = x3_sched_count();
   x3 = false;
   t = tile;
   if (patch) *patch = false;
+  if (stream) *stream = false;
   if (math != PLD_MATH_BF16X3) return;
   if (tile >= nx) {
     t = tile - nx;
@@ -855,7 +860,10 @@ static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t,
     return;
   }
   x3 = true;
-  if (tile >= 2 * n3) {
+  if (tile >= 2 * n3 + np) {  // tile stream of cfg tile - (2 n3 + np); callers that cannot
+    t = stream ? tile - 2 * n3 - np : -1;  // run it take the default tile
+    if (stream) *stream = true;
+  } else if (tile >= 2 * n3) {
     t = patch ? tile - 2 * n3 : -1;
     if (patch) *patch = true;
   }
@@ -920,6 +928,36 @@ static void x3_fwd_plan(long M, long N, long K, long ktiles, int tile, int& cfg,
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
 
+// tile-stream plan: T tiles of nk K-steps on occ resident workgroups per CU. As many tiles as
+// resident slots or more: whole tiles per workgroup, balanced (the pipeline runs on from tile to
+// tile); fewer: the (tile, K-step) space cut evenly over the slots, >= 16 K-steps each
+// (stream-K: cut tiles are summed by the fixup kernel). Returns the grid; sets p.sk_*.
+static int x3_stream_plan(GemmConvParams& p, int cfg, long ktiles) {
+  int bm, bn, tm, tn, occ;
+  pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+  const long tiles = (long)cdiv(p.M, bm) * cdiv(p.N, bn);
+  const long slots = 256L * occ;
+  p.sk_nk = (int)ktiles;
+  p.sk_tiles = (int)tiles;
+  p.sk_nnb = (int)cdiv(p.N, bn);
+  long G;
+  if (tiles >= slots) {
+    const long per = cdiv(tiles, slots);
+    G = cdiv(tiles, per);
+    p.sk_align = 1;
+  } else {
+    G = std::min<long>(slots, std::max<long>(tiles, tiles * ktiles / 16));
+    p.sk_align = (G == tiles) ? 1 : 0;
+  }
+  return (int)G;
+}
+static size_t x3_stream_slab_bytes(const GemmConvParams& p, int cfg, int G) {
+  if (p.sk_align) return 0;
+  int bm, bn, tm, tn, occ;
+  pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+  return sizeof(float) * 2 * (size_t)G * bm * bn;
+}
+
 // split-K plan for a forward / dgrad GEMM under schedule `tile`: enough workgroups for ~3 per
 // CU, >= 16 K-steps each; the split-K schedules (tile >= kNumCfg) only
 static void fwd_split_plan(long M, long N, long K, int tile, int& cfg, int& splits,
@@ -964,9 +1002,14 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
                         size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
   bool x3;
-  bool patch;
+  bool patch, stream;
   resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
-                tile, &patch);
+                tile, &patch, &stream);
+  const long in_bytes = (long)p.n * p.h * p.w * std::max(p.c1, p.c2) * 4;
+  if (stream && (p.in_scale || in_bytes >= MAX_RECORDS)) {  // stream: no prologue, whole-tensor
+    stream = false;                                         // descriptors
+    tile = -1;
+  }
   if (patch && !pld__x3_patch_ok(&p, tile)) {  // patch schedule on another shape: default tile
     patch = false;
     tile = -1;
@@ -989,6 +1032,21 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
     if (patch) return pld__x3_patch_launch(&p, tile, st);
     p.kc_tap = x3_kc_tap(p.kh * p.kw, p.c1, p.c2);
     p.kc1 = (int)cdiv(p.c1, X3_BK);
+    if (stream) {
+      cfg = tile;
+      const int G = x3_stream_plan(p, cfg, x3_ktiles(p.kc_tap, p.kh * p.kw, p.K));
+      const size_t need = x3_stream_slab_bytes(p, cfg, G);
+      PLD_CHECK_ARG(need == 0 || (ws && ws_bytes >= need),
+                    "%s: tile-stream workspace %zu < %zu bytes", who, ws_bytes, need);
+      PLD_CHECK_ARG((long)p.N * p.K * 4 < MAX_RECORDS, "%s: filter too large", who);
+      p.sk_slab = need ? (float*)ws : nullptr;
+      p.ktiles_per_split = 0;
+      p.zstride = 0;
+      int bm, bn, tm, tn, occ;
+      pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
+      fwd_stats_attach(p, bm, tm);
+      return pld__x3_launch(&p, MODE_FWD, 1, cfg, G, st);
+    }
     x3_fwd_plan(p.M, p.N, p.K, x3_ktiles(p.kc_tap, p.kh * p.kw, p.K), tile, cfg, splits, kt_per);
     int bm, bn, tm, tn, occ;
     pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
@@ -998,7 +1056,7 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
     fwd_split_plan(p.M, p.N, p.K, tile, cfg, splits, kt_per);
   }
   auto launch = [&](GemmConvParams& q, int sp) {
-    return x3 ? pld__x3_launch(&q, MODE_FWD, sp, cfg, st)
+    return x3 ? pld__x3_launch(&q, MODE_FWD, sp, cfg, 0, st)
               : launch_igemm<MODE_FWD>(q, vec, vec16, sp, cfg, st);
   };
   if (x3) {
@@ -1043,12 +1101,22 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
 static size_t fwd_ws_bytes(long M, long N, long K, int taps, int c1, int c2, int tile,
                            int math = 0, bool geom = false, bool have_split = true) {
   int cfg, splits, kt_per;
-  bool x3;
-  resolve_sched(math, geom, tile, x3, tile);
-  if (x3)
-    x3_fwd_plan(M, N, K, x3_ktiles(x3_kc_tap(taps, c1, c2), taps, K), tile, cfg, splits, kt_per);
-  else fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
-  size_t b = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  bool x3, stream;
+  resolve_sched(math, geom, tile, x3, tile, nullptr, &stream);
+  size_t b;
+  if (stream) {  // (an input prologue runs on the default tile: no workspace either way)
+    GemmConvParams q{};
+    q.M = (int)M;
+    q.N = (int)N;
+    const int G = x3_stream_plan(q, tile, x3_ktiles(x3_kc_tap(taps, c1, c2), taps, K));
+    b = x3_stream_slab_bytes(q, tile, G);
+  } else {
+    if (x3)
+      x3_fwd_plan(M, N, K, x3_ktiles(x3_kc_tap(taps, c1, c2), taps, K), tile, cfg, splits,
+                  kt_per);
+    else fwd_split_plan(M, N, K, tile, cfg, splits, kt_per);
+    b = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+  }
   if (x3 && !have_split) b = (b + 255) / 256 * 256 + x3_split_bytes(N, K);
   return b;
 }
@@ -1211,18 +1279,18 @@ extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_oh
 extern "C" int pld_conv_num_tiles(void) { return kNumTiles; }
 
 extern "C" int pld_conv_num_schedules(int math) {
-  return math == PLD_MATH_BF16X3 ? 2 * pld__x3_num_cfg() + pld__x3_num_patch() + kNumTiles
-                                 : kNumTiles;
+  return math == PLD_MATH_BF16X3 ? x3_sched_count() + kNumTiles : kNumTiles;
 }
 
 extern "C" int pld_conv_schedule_class(int math, int idx) {
   if (idx < 0 || idx >= pld_conv_num_schedules(math)) return -1;
   const int nf = kNumTiles / 2;  // fp32: [tiles | tiles x split-K]
   if (math != PLD_MATH_BF16X3) return idx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
-  const int n3 = pld__x3_num_cfg(), nx = 2 * n3 + pld__x3_num_patch();
+  const int n3 = pld__x3_num_cfg(), np = pld__x3_num_patch(), nx = x3_sched_count();
   if (idx < n3) return PLD_SCHED_X3;
   if (idx < 2 * n3) return PLD_SCHED_X3_SPLIT;
-  if (idx < nx) return PLD_SCHED_X3_PATCH;
+  if (idx < 2 * n3 + np) return PLD_SCHED_X3_PATCH;
+  if (idx < nx) return PLD_SCHED_X3_STREAM;
   return idx - nx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
 }
 
@@ -1233,14 +1301,18 @@ extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
   if (cls < 0 || idx >= 128) return nullptr;
   char* out = names[math == PLD_MATH_BF16X3 ? 1 : 0][idx];
   if (out[0]) return out;
-  const int n3 = pld__x3_num_cfg();
-  const int nx = math == PLD_MATH_BF16X3 ? 2 * n3 + pld__x3_num_patch() : 0;
+  const int n3 = pld__x3_num_cfg(), np = pld__x3_num_patch();
+  const int nx = math == PLD_MATH_BF16X3 ? x3_sched_count() : 0;
   int bm = 0, bn = 0, tm, tn, occ;
   switch (cls) {
     case PLD_SCHED_X3:
     case PLD_SCHED_X3_SPLIT:
       pld__x3_cfg_dims(idx % n3, &bm, &bn, &tm, &tn, &occ);
       snprintf(out, 24, "%s/%dx%d", cls == PLD_SCHED_X3 ? "x3" : "x3split", bm, bn);
+      break;
+    case PLD_SCHED_X3_STREAM:
+      pld__x3_cfg_dims(idx - 2 * n3 - np, &bm, &bn, &tm, &tn, &occ);
+      snprintf(out, 24, "x3stream/%dx%d", bm, bn);
       break;
     case PLD_SCHED_X3_PATCH:
       snprintf(out, 24, "x3patch/%d", pld__x3_patch_bn(idx - 2 * n3));
@@ -1463,20 +1535,40 @@ static bool wgrad_patch_geom(const pld_conv_args* a) {
          a->pad_t <= 2 && a->pad_l >= 0 && a->pad_l <= 2;
 }
 
+// stream_grid (optional): > 0 when the call runs the tile stream with that many workgroups
+// (stream_p then holds its sk_* plan)
 static void wgrad_plan(const pld_conv_args* a, int& M, int& N, long& K, int& splits,
-                       int& kt_per, int& cfg, bool& x3, bool* patch_out = nullptr) {
+                       int& kt_per, int& cfg, bool& x3, bool* patch_out = nullptr,
+                       int* stream_grid = nullptr, GemmConvParams* stream_p = nullptr) {
   M = a->kh * a->kw * (a->c1 + a->c2);
   N = a->cout;
   K = (long)a->n * a->oh * a->ow;
   int tile;
-  bool patch;
+  bool patch, stream;
   resolve_sched(a->math, x3_wgrad_geom(a->c1, a->c2, a->cout, a->in_scale != nullptr), a->tile,
-                x3, tile, &patch);
+                x3, tile, &patch, &stream);
   if (patch && !wgrad_patch_geom(a)) {
     patch = false;
     tile = -1;
   }
   if (patch_out) *patch_out = patch;
+  if (stream_grid) *stream_grid = 0;
+  if (stream) {  // whole-tensor descriptors: operands under 2 GiB
+    const long in_bytes = (long)a->n * a->h * a->w * std::max(a->c1, a->c2) * 4;
+    if (in_bytes < MAX_RECORDS && K * N * 4 < MAX_RECORDS) {
+      GemmConvParams q{};
+      q.M = M;
+      q.N = N;
+      cfg = tile;
+      splits = 1;
+      kt_per = 0;
+      const int G = x3_stream_plan(q, cfg, (K + X3_BK - 1) / X3_BK);
+      if (stream_grid) *stream_grid = G;
+      if (stream_p) *stream_p = q;
+      return;
+    }
+    tile = -1;
+  }
   if (patch) {  // patch schedule: workgroups = chunks x cout tiles x splits, ~512 in all
     const long tiles = (long)cdiv(a->ow, 32) * cdiv(a->oh, pld__x3_patch_wgrad_th(N)) * a->n;
     const long blocks = (long)(cdiv(a->c1, 32) + cdiv(a->c2, 32)) *
@@ -1531,10 +1623,12 @@ extern "C" size_t pld_conv2d_wgrad_workspace_size(const pld_conv_args* a) {
     return 0;
   if (pld__scalar1x1_eligible(a)) return pld__scalar1x1_wgrad_ws();
   if (pld__skinny_eligible(a)) return pld__skinny_wgrad_ws(a);
-  int M, N, splits, kt, cfg;
+  int M, N, splits, kt, cfg, G;
   long K;
   bool x3;
-  wgrad_plan(a, M, N, K, splits, kt, cfg, x3);
+  GemmConvParams q{};
+  wgrad_plan(a, M, N, K, splits, kt, cfg, x3, nullptr, &G, &q);
+  if (G > 0) return x3_stream_slab_bytes(q, cfg, G);
   return wgrad_ws_bytes(splits, M, N);
 }
 
@@ -1556,12 +1650,14 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
                   ws_bytes, need);
     return pld__skinny_wgrad(a, dy, dw, accumulate, ws, stream);
   }
-  int M, N, splits, kt_per, cfg;
+  int M, N, splits, kt_per, cfg, sk_grid;
   long K;
   bool x3, patch;
-  wgrad_plan(a, M, N, K, splits, kt_per, cfg, x3, &patch);
+  GemmConvParams sk{};
+  wgrad_plan(a, M, N, K, splits, kt_per, cfg, x3, &patch, &sk_grid, &sk);
   PLD_CHECK_ARG(K < (1L << 31), "pld_conv2d_wgrad: too many pixels");
-  const size_t need = wgrad_ws_bytes(splits, M, N);
+  const size_t need = sk_grid > 0 ? x3_stream_slab_bytes(sk, cfg, sk_grid)
+                                  : wgrad_ws_bytes(splits, M, N);
   PLD_CHECK_ARG(ws_bytes >= need && (need == 0 || ws),
                 "pld_conv2d_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
   p.bmat = dy;
@@ -1592,9 +1688,18 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
                       (long)a->oh * a->ow * N * 4 < MAX_RECORDS,
                   "pld_conv2d_wgrad: image too large for 32-bit buffer offsets");
     rc = pld__x3_patch_wgrad_launch(&p, splits, st);
+  } else if (x3 && sk_grid > 0) {
+    PLD_CHECK_ARG(vec, "pld_conv2d_wgrad: bf16x3 operands must be 16-byte aligned");
+    p.sk_nk = sk.sk_nk;
+    p.sk_tiles = sk.sk_tiles;
+    p.sk_nnb = sk.sk_nnb;
+    p.sk_align = sk.sk_align;
+    p.sk_slab = sk.sk_align ? nullptr : (float*)ws;
+    p.ktiles_per_split = 0;
+    rc = pld__x3_launch(&p, MODE_WGRAD, 1, cfg, sk_grid, st);
   } else if (x3) {
     PLD_CHECK_ARG(vec, "pld_conv2d_wgrad: bf16x3 operands must be 16-byte aligned");
-    rc = pld__x3_launch(&p, MODE_WGRAD, splits, cfg, st);
+    rc = pld__x3_launch(&p, MODE_WGRAD, splits, cfg, 0, st);
   } else {
     rc = launch_igemm<MODE_WGRAD>(p, vec, false, splits, cfg, st);
   }

@@ -32,511 +32,12 @@
 //     into a [k = pixel][channel] image that the consumers read with ds_read_b64_tr_b16
 //     (hardware transpose) into the k-contiguous MFMA fragments.
 #include <algorithm>
-#include <type_traits>
 #include <cstdlib>
 
-#include "conv_common.h"
+#include "conv_x3_core.h"
 
 namespace pld {
 namespace x3 {
-
-constexpr int BK = 32;
-
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// two floats -> packed bf16 (hi pair, lo pair)
-__device__ __forceinline__ void split2(float x, float y, unsigned& hi, unsigned& lo) {
-  const bf16x2 h = {(__bf16)x, (__bf16)y};
-  hi = __builtin_bit_cast(unsigned, h);
-  const float xr = x - __uint_as_float(hi << 16);
-  const float yr = y - __uint_as_float(hi & 0xffff0000u);
-  const bf16x2 l = {(__bf16)xr, (__bf16)yr};
-  lo = __builtin_bit_cast(unsigned, l);
-}
-
-// byte offset of 16-byte k-chunk `c` of row `r` inside one plane. The chunk is stored in slot
-// c ^ g(r), g(r) = (r1 ^ r3) | r2 << 1 (r_i = bit i of r): conflict-free for the ds_read_b128
-// fragment reads (16-lane groups of rows, one chunk) and for the producers' ds_write_b128 of 8
-// consecutive rows (searched exhaustively over linear GF(2) swizzles of the row bits).
-__device__ __forceinline__ int chunk_off(int r, int c) {
-  const int g = (((r >> 1) ^ (r >> 3)) & 1) | ((r >> 1) & 2);
-  return r * 64 + 16 * (c ^ g);
-}
-
-__device__ __forceinline__ bf16x8 lds_frag(const unsigned char* plane, int r, int c) {
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + chunk_off(r, c)));
-}
-
-// WGRAD image: [32 k rows][R columns] bf16 per plane. A transposed read (4 consecutive k rows x
-// 32 bytes per 16-lane group, the second group 32 bytes further) must touch distinct banks:
-// with a row pitch that is a multiple of 256 B (R = 32, 64, 128, 256) the 32-byte column blocks
-// are XOR-swizzled by 2(k & 3); a pitch of 320, 192 or 448 B (R = 160, 96, 224) already puts the
-// four rows 16 banks apart; R = 192 (384 B: rows alternate between two bank offsets) swaps block
-// pairs on k & 2.
-template <int R>
-__device__ __forceinline__ int tr_off(int k, int col) {
-  constexpr int NB = R / 16;  // 32-byte blocks per row
-  static_assert(R % 32 == 0 && R >= 32 && R <= 256, "WGRAD image width");
-  int sw = 0;
-  if constexpr ((NB & (NB - 1)) == 0) sw = ((k & 3) << 1) & (NB - 1);
-  else if constexpr (NB == 12) sw = k & 2;
-  const int b = (col >> 4) ^ sw;
-  return k * (2 * R) + b * 32 + (col & 15) * 2;
-}
-
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4s lds_v4s;
-
-// 32x32x16 operand fragment from a [k][col] image with ds_read_b64_tr_b16: lane l needs
-// column c0 + (l & 31), k = 16 s + 8 (l >> 5) .. +7; each 16-lane group reads 4 k-rows x 16
-// columns per instruction (lane 4q+p supplies row q, columns 4p..4p+3) and receives its column
-template <int R>
-__device__ __forceinline__ bf16x8 lds_frag_tr(const unsigned char* plane, int c0, int s,
-                                              int lane) {
-  const int i16 = lane & 15, grp = (lane >> 4) & 1, h = lane >> 5;
-  const int k = 16 * s + 8 * h + (i16 >> 2);
-  const int col = c0 + 16 * grp + 4 * (i16 & 3);
-  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4s*)(plane + tr_off<R>(k, col)));
-  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_v4s*)(plane + tr_off<R>(k + 4, col)));
-  const v4s v[2] = {lo, hi};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// LDS hand-off between the producer and consumer waves: the writer's ds_writes are complete
-// (lgkmcnt) before the barrier; no vmcnt wait, so the producers' next global loads stay in
-// flight across it. The empty asm statements keep the compiler from moving LDS accesses across.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int BM, int BN>
-struct X3Smem {
-  static constexpr int A_PLANE = BM * 64, B_PLANE = BN * 64;  // bytes of one bf16 plane
-  static constexpr int A_BYTES = 2 * A_PLANE, B_BYTES = 2 * B_PLANE;
-  static constexpr int BYTES = 2 * (A_BYTES + B_BYTES);         // double-buffered
-  __device__ static unsigned char* a(unsigned char* s, int buf) { return s + buf * A_BYTES; }
-  __device__ static unsigned char* b(unsigned char* s, int buf) {
-    return s + 2 * A_BYTES + buf * B_BYTES;
-  }
-};
-
-// ---------------------------------------------------------------------------- producer
-// Four waves (pw = 0..3) stage K-steps: global fp32 -> bf16 hi/lo -> LDS. Every K-step issues
-// the same, unconditional set of loads (the concat's second source is a template parameter, the
-// last steps re-fetch the final tile), so the compiler can count the loads in flight and wait
-// for exactly one stage (vmcnt(N)), never draining the prefetch (vmcnt(0)).
-template <int BM, int BN, int MODE, bool CAT, bool TI, bool PRO>
-__device__ __forceinline__ void x3_producer(const GemmConvParams& p, unsigned char* smem,
-                                            int kt_begin, int kt_end, int pw, int lane, int mb,
-                                            int nb) {
-  using S = X3Smem<BM, BN>;
-  const int ptid = pw * 64 + lane;
-  const int m0 = mb * BM;
-  const int n0 = nb * BN;
-
-  // x1/x2 addressed relative to the first image this workgroup touches (32-bit offsets)
-  int img_base, pix_base = 0;
-  if (MODE == MODE_FWD) {
-    img_base = (int)p.dOH.div(p.dOW.div((uint32_t)m0));
-  } else {
-    pix_base = kt_begin * BK;
-    img_base = (int)p.dOH.div(p.dOW.div((uint32_t)min(pix_base, p.K - 1)));
-  }
-  const long img_elems = (long)p.h * p.w;
-  const __amdgpu_buffer_rsrc_t rs1 =
-      make_rsrc(p.x1 + img_base * img_elems * p.c1, (p.n - img_base) * img_elems * p.c1 * 4);
-  const __amdgpu_buffer_rsrc_t rs2 =
-      CAT ? make_rsrc(p.x2 + img_base * img_elems * p.c2, (p.n - img_base) * img_elems * p.c2 * 4)
-          : rs1;
-  // FWD: B is the pre-split filter (pld_filter_split layout); WGRAD: B = dY fp32
-  const __amdgpu_buffer_rsrc_t rsb =
-      (MODE == MODE_FWD)
-          ? make_rsrc(p.bsplit, (long)p.N * p.K * 4)
-          : make_rsrc(p.bmat + (long)pix_base * p.N, (long)(p.K - pix_base) * p.N * 4);
-
-  // FWD: full-line staging. A wave-instruction covers 8 rows x 128 B: lane = (row lr = lane/8,
-  // 4-k group ks = lane%8); producer wave pw owns rows [pw BM/4, (pw+1) BM/4) of A and
-  // [pw BN/4, ...) of B, in groups of 8. B lanes 0-31 stage the hi halves, 32-63 the lo halves
-  // of 8 rows x 4 chunks (chunk = 32 B: [8 hi][8 lo] bf16).
-  static_assert(MODE != MODE_FWD || (BM % 32 == 0 && BN % 32 == 0), "FWD tiles: rows % 32");
-  constexpr int FA = BM / 32, FB = BN / 32;
-  const int lr = lane >> 3, ks = lane & 7;
-  const int br = lane & 31, half = lane >> 5;
-  // per A row: pixel index of tap (0,0) relative to the descriptor base, and the taps that land
-  // inside the image (bit t, taps <= 32); per B row: byte offset and validity
-  int a_base[FA];
-  unsigned a_taps[FA];
-  unsigned b_off[FB];
-  bool b_ok[FB];
-  // WGRAD: a thread owns 16 consecutive columns (fixed channels: one tap, one source, since
-  // C, c1 % 16 == 0) of P pixel slots g, g + G, ... of each K-step (NQ = R/16 threads per pixel
-  // row, G = floor(256/NQ) rows per pass, P = ceil(32/G); threads past row 31, and the
-  // 256 mod NQ threads past the last full pass, idle). One pixel decomposition serves 16
-  // channels; lanes run along a pixel row: 64-byte coalesced loads, and each thread fills one
-  // whole 32-byte block of the [k][col] image read back transposed.
-  constexpr int NQA = BM / 16, NQB = BN / 16;
-  constexpr int GA = 256 / NQA, GB = 256 / NQB;
-  constexpr int PA = (BK + GA - 1) / GA, PB = (BK + GB - 1) / GB;
-  static_assert(MODE == MODE_FWD || (BM >= 32 && BN >= 32 && BM <= 256 && BN <= 256),
-                "WGRAD tile columns must be 32..256");
-  int w_ty = 0, w_tx = 0, w_ci = 0;
-  bool w_ok = false, w_in1 = true;
-  int w_cs = 0;                // WGRAD concat: this thread's source channel count and
-  const float* w_src = p.x1;   // its first channel's address in the workgroup's first image
-
-  if (MODE == MODE_FWD) {
-#pragma unroll
-    for (int j = 0; j < FA; ++j) {
-      const int r = pw * (BM / 4) + 8 * j + lr;
-      const int m = m0 + r;
-      const bool mok = m < p.M;
-      const int mm = mok ? m : m0;
-      const uint32_t q = p.dOW.div((uint32_t)mm);
-      const int ox = mm - (int)q * p.ow;
-      const uint32_t img = p.dOH.div(q);
-      const int oy = (int)q - (int)img * p.oh;
-      const int iy0 = oy * p.sh - p.pt, ix0 = ox * p.sw - p.pl;
-      a_base[j] = (((int)img - img_base) * p.h + iy0) * p.w + ix0;
-      unsigned t = 0;
-      for (int ty = 0; ty < p.kh; ++ty)
-        for (int tx = 0; tx < p.kw; ++tx)
-          t |= (unsigned)(mok && (unsigned)(iy0 + ty) < (unsigned)p.h &&
-                          (unsigned)(ix0 + tx) < (unsigned)p.w) << (ty * p.kw + tx);
-      a_taps[j] = t;
-    }
-#pragma unroll
-    for (int j = 0; j < FB; ++j) {
-      const int nn = n0 + pw * (BN / 4) + 8 * j + (br >> 2);
-      b_ok[j] = nn < p.N;
-      b_off[j] = (unsigned)(b_ok[j] ? nn : 0) * (unsigned)p.K * 4u + 16u * half;
-    }
-  } else {
-    const int i = m0 + 16 * (ptid % NQA);
-    w_ok = i < p.M;
-    const int ii = w_ok ? i : 0;
-    const uint32_t tap = p.dC.div((uint32_t)ii);
-    w_ci = ii - (int)tap * p.C;
-    const uint32_t ty = p.dKW.div(tap);
-    w_ty = (int)ty;
-    w_tx = (int)tap - (int)ty * p.kw;
-    w_in1 = w_ci < p.c1;
-    w_cs = w_in1 ? p.c1 : p.c2;
-    w_src = w_in1 ? p.x1 + img_base * img_elems * p.c1 + w_ci
-                  : p.x2 + img_base * img_elems * p.c2 + (w_ci - p.c1);
-  }
-
-  constexpr int RA = (MODE == MODE_FWD) ? FA : 4 * PA;  // float4 staging registers, A
-  constexpr int RB = (MODE == MODE_FWD) ? FB : 4 * PB;  // and B
-  struct Stage {  // one K-step in flight
-    float4 ra[RA], rb[RB];
-    float4 ps, pt;  // PRO: this lane's 4 channels' prologue scale / shift
-    unsigned okm;   // PRO: bit j = A row j's element lies inside the image (else it stays 0)
-  };
-  static_assert(!PRO || (MODE == MODE_FWD && !CAT), "prologue: one-source FWD view only");
-
-  auto load_tile = [&](int kt, Stage& st) {
-    const int k0 = kt * BK;
-    if (MODE == MODE_FWD && TI) {
-      // tap-inner order: K-step kt = (chunk kq, tap) with the chunks of x1 first, then x2, each
-      // 32 channels of ONE source (ragged last chunk masked): one load per element and the
-      // source's descriptor picked per step (wave-uniform), where the linear order needs both
-      const int kq = (int)p.dTaps.div((uint32_t)kt);
-      const int tap = kt - kq * p.kh * p.kw;
-      const bool s2 = CAT && kq >= p.kc1;
-      const int chb = (s2 ? kq - p.kc1 : kq) * BK;  // first channel of the chunk in its source
-      const int cs = s2 ? p.c2 : p.c1;
-      const __amdgpu_buffer_rsrc_t rs = s2 ? rs2 : rs1;
-      const int c = chb + 4 * ks;
-      const bool kin = c < cs;
-      const int ty = (int)p.dKW.div((uint32_t)tap);
-      const int toff = ty * p.w + (tap - ty * p.kw);  // pixel offset of the tap
-      unsigned okm = 0;
-#pragma unroll
-      for (int j = 0; j < FA; ++j) {
-        const bool ok = kin && ((a_taps[j] >> tap) & 1u);
-        okm |= (unsigned)ok << j;
-        st.ra[j] = bload4(rs, ok ? (unsigned)(((a_base[j] + toff) * cs + c) * 4) : OOB);
-      }
-      if constexpr (PRO) {  // unconditional loads (clamped channel): no branch around them
-        const int cc = kin ? c : 0;
-        st.ps = *reinterpret_cast<const float4*>(p.in_scale + cc);
-        st.pt = *reinterpret_cast<const float4*>(p.in_shift + cc);
-        st.okm = okm;
-      }
-      const int cb8 = chb + 8 * (br & 3);  // this lane's 8-k chunk of the filter
-      const int kc = tap * p.C + (s2 ? p.c1 : 0) + cb8;
-      const bool kcin = cb8 < cs;
-#pragma unroll
-      for (int j = 0; j < FB; ++j)
-        st.rb[j] = bload4(rsb, (b_ok[j] && kcin) ? b_off[j] + 4u * (unsigned)kc : OOB);
-    } else if (MODE == MODE_FWD) {
-      const int k = k0 + 4 * ks;  // this lane's 4 consecutive k (C % 8 == 0: one tap, one source)
-      const bool kin = k < p.K;
-      const int kk = kin ? k : 0;
-      const int tap = (int)p.dC.div((uint32_t)kk);
-      const int ci = kk - tap * p.C;
-      const int ty = (int)p.dKW.div((uint32_t)tap);
-      const int toff = ty * p.w + (tap - ty * p.kw);  // pixel offset of the tap
-      const bool src2 = CAT && ci >= p.c1;
-      const int cs = src2 ? p.c2 : p.c1;
-      const int cb = src2 ? ci - p.c1 : ci;
-      unsigned okm = 0;
-#pragma unroll
-      for (int j = 0; j < FA; ++j) {
-        const bool ok = kin && ((a_taps[j] >> tap) & 1u);
-        okm |= (unsigned)ok << j;
-        const unsigned off = (unsigned)(((a_base[j] + toff) * cs + cb) * 4);
-        if (CAT)  // both sources, the other one out of range (reads as 0)
-          st.ra[j] = add4(bload4(rs1, (ok && !src2) ? off : OOB), bload4(rs2, (ok && src2) ? off : OOB));
-        else
-          st.ra[j] = bload4(rs1, ok ? off : OOB);
-      }
-      if constexpr (PRO) {
-        const int cc = kin ? cb : 0;
-        st.ps = *reinterpret_cast<const float4*>(p.in_scale + cc);
-        st.pt = *reinterpret_cast<const float4*>(p.in_shift + cc);
-        st.okm = okm;
-      }
-      const int kc = k0 + 8 * (br & 3);
-      const bool kcin = kc < p.K;
-#pragma unroll
-      for (int j = 0; j < FB; ++j)
-        st.rb[j] = bload4(rsb, (b_ok[j] && kcin) ? b_off[j] + 4u * (unsigned)kc : OOB);
-    } else {
-      const int ga = ptid / NQA;
-#pragma unroll
-      for (int j = 0; j < PA; ++j) {
-        const int slot = ga + GA * j;
-        const int pix = k0 + slot;
-        const bool rok = ga < GA && slot < BK && pix < p.K;
-        const int pp = rok ? pix : pix_base;
-        const uint32_t q = p.dOW.div((uint32_t)pp);
-        const int ox = pp - (int)q * p.ow;
-        const uint32_t img = p.dOH.div(q);
-        const int oy = (int)q - (int)img * p.oh;
-        const int ir = ((int)img - img_base) * p.h;
-        const int iy = oy * p.sh - p.pt + w_ty, ix = ox * p.sw - p.pl + w_tx;
-        const bool ok = rok && w_ok && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-        const int px = (ir + iy) * p.w + ix;
-        if (CAT) {  // this thread's source is fixed: one (per-lane address) load per element;
-                    // masked lanes re-read their first 16 channels and zero the data
-          const float4* a = reinterpret_cast<const float4*>(w_src + (ok ? px * w_cs : 0));
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float4 v = a[u];
-            st.ra[4 * j + u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        } else {
-          const unsigned o1 = ok ? (unsigned)((px * p.c1 + w_ci) * 4) : OOB;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) st.ra[4 * j + u] = bload4(rs1, o1 == OOB ? OOB : o1 + 16 * u);
-        }
-      }
-      const int gb = ptid / NQB;
-      const int n = n0 + 16 * (ptid % NQB);
-#pragma unroll
-      for (int j = 0; j < PB; ++j) {
-        const int slot = gb + GB * j;
-        const int pix = k0 + slot;
-        const bool ok = gb < GB && slot < BK && pix < p.K && n < p.N;
-        const unsigned o = ok ? (unsigned)(((pix - pix_base) * p.N + n) * 4) : OOB;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) st.rb[4 * j + u] = bload4(rsb, o == OOB ? OOB : o + 16 * u);
-      }
-    }
-  };
-
-  // 16 columns of one k row -> one 32-byte block in each plane of the [k][col] image
-  auto store_row16 = [&](unsigned char* plane, int plane_bytes, auto rcols, int k, int col,
-                         const float4* v) {
-    unsigned h[8], l[8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      split2(v[u].x, v[u].y, h[2 * u], l[2 * u]);
-      split2(v[u].z, v[u].w, h[2 * u + 1], l[2 * u + 1]);
-    }
-    const int o = tr_off<decltype(rcols)::value>(k, col);
-    *reinterpret_cast<u32x4*>(plane + o) = u32x4{h[0], h[1], h[2], h[3]};
-    *reinterpret_cast<u32x4*>(plane + o + 16) = u32x4{h[4], h[5], h[6], h[7]};
-    *reinterpret_cast<u32x4*>(plane + plane_bytes + o) = u32x4{l[0], l[1], l[2], l[3]};
-    *reinterpret_cast<u32x4*>(plane + plane_bytes + o + 16) = u32x4{l[4], l[5], l[6], l[7]};
-  };
-
-  auto store_tile = [&](int buf, const Stage& st) {
-    unsigned char* A = S::a(smem, buf);
-    unsigned char* B = S::b(smem, buf);
-    if (MODE == MODE_FWD) {
-      const int ob = 8 * (ks & 1);  // byte offset of this lane's 4 k inside its 16-byte chunk
-#pragma unroll
-      for (int j = 0; j < FA; ++j) {
-        const int r = pw * (BM / 4) + 8 * j + lr;
-        float4 v = st.ra[j];
-        if constexpr (PRO)
-          v = ((st.okm >> j) & 1u) ? prologue4(p.in_act, v, st.ps, st.pt)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        unsigned h0, l0, h1, l1;
-        split2(v.x, v.y, h0, l0);
-        split2(v.z, v.w, h1, l1);
-        const int o = chunk_off(r, ks >> 1) + ob;
-        *reinterpret_cast<u32x2*>(A + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(A + S::A_PLANE + o) = u32x2{l0, l1};
-      }
-#pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        const int r = pw * (BN / 4) + 8 * j + (br >> 2);
-        *reinterpret_cast<float4*>(B + half * S::B_PLANE + chunk_off(r, br & 3)) = st.rb[j];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < PA; ++j) {
-        const int slot = ptid / NQA + GA * j;
-        if (ptid / NQA < GA && slot < BK)
-          store_row16(A, S::A_PLANE, std::integral_constant<int, BM>{}, slot,
-                      16 * (ptid % NQA), &st.ra[4 * j]);
-      }
-#pragma unroll
-      for (int j = 0; j < PB; ++j) {
-        const int slot = ptid / NQB + GB * j;
-        if (ptid / NQB < GB && slot < BK)
-          store_row16(B, S::B_PLANE, std::integral_constant<int, BN>{}, slot,
-                      16 * (ptid % NQB), &st.rb[4 * j]);
-      }
-    }
-  };
-
-  // Two register stages: K-step i+1 is stored while i runs on the MFMAs and its registers are
-  // refilled with step i+3 (clamped to the last step: a harmless re-fetch) — every global load
-  // has two K-steps of MFMA work to land. Barriers (match the consumer): 1 + n.
-  const int n = kt_end - kt_begin;
-  if (n <= 0) {
-    lds_barrier();
-    return;
-  }
-  const int last = kt_end - 1;
-  Stage s0, s1;
-  load_tile(kt_begin, s0);
-  store_tile(0, s0);
-  load_tile(min(kt_begin + 1, last), s0);
-  load_tile(min(kt_begin + 2, last), s1);
-  lds_barrier();
-  for (int i = 0;; i += 2) {
-    store_tile(1, s0);  // step i+1 (odd) -> buffer 1 (unused past the end)
-    load_tile(min(kt_begin + i + 3, last), s0);
-    lds_barrier();
-    if (i + 1 >= n) break;
-    store_tile(0, s1);  // step i+2 (even) -> buffer 0
-    load_tile(min(kt_begin + i + 4, last), s1);
-    lds_barrier();
-    if (i + 2 >= n) break;
-  }
-}
-
-// ---------------------------------------------------------------------------- consumer
-template <int BM, int BN, int WM, int WN, int MODE>
-__device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned char* smem,
-                                            int kt_begin, int kt_end, int wave, int lane, int mb,
-                                            int nb, int zb) {
-  using S = X3Smem<BM, BN>;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
-  const int wm = wave / WN, wn = wave % WN;
-  const int h = lane >> 5, l32 = lane & 31;
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  lds_barrier();
-  for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const int buf = (kt - kt_begin) & 1;
-    const unsigned char* A = S::a(smem, buf);
-    const unsigned char* B = S::b(smem, buf);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        if constexpr (MODE == MODE_WGRAD) {
-          ah[a] = lds_frag_tr<BM>(A, wm * WTM + a * 32, s, lane);
-          al[a] = lds_frag_tr<BM>(A + S::A_PLANE, wm * WTM + a * 32, s, lane);
-        } else {
-          const int r = wm * WTM + a * 32 + l32;
-          ah[a] = lds_frag(A, r, 2 * s + h);
-          al[a] = lds_frag(A + S::A_PLANE, r, 2 * s + h);
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        if constexpr (MODE == MODE_WGRAD) {
-          bh[b] = lds_frag_tr<BN>(B, wn * WTN + b * 32, s, lane);
-          bl[b] = lds_frag_tr<BN>(B + S::B_PLANE, wn * WTN + b * 32, s, lane);
-        } else {
-          const int r = wn * WTN + b * 32 + l32;
-          bh[b] = lds_frag(B, r, 2 * s + h);
-          bl[b] = lds_frag(B + S::B_PLANE, r, 2 * s + h);
-        }
-      }
-      // keep the substep's fragment reads together ahead of its MFMAs (one LDS wait per
-      // substep instead of the scheduler's register-saving read-wait-MFMA interleave)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-        }
-    }
-    lds_barrier();
-  }
-  store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane, zb);
-}
-
-// 512 threads: waves 0-3 consume (LDS fragments -> MFMA), waves 4-7 produce the next K-step
-// (global loads, prologue, hi/lo split, LDS stores) — a VALU-heavy wave and an MFMA-heavy
-// wave share each SIMD, so the split overlaps the matrix work.
-template <int BM, int BN, int WM, int WN, int MODE, bool CAT, bool TI, bool PRO = false>
-__global__ __launch_bounds__((WM * WN + 4) * 64) void conv_x3_kernel(GemmConvParams p) {
-  static_assert(WM * WN == 4, "4 consumer waves");
-  static_assert((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[X3Smem<BM, BN>::BYTES];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (b, b+8, ... share
-  // one), so give each XCD a contiguous run of tiles, N fastest, then M, then the K split:
-  // the N tiles of one M tile (same A rows) and neighbouring M tiles (overlapping im2col
-  // halos) share that XCD's L2. Bijective for any grid size (speed only, never correctness).
-  const int nmb = gridDim.x, nnb = gridDim.y;
-  const int nwg = nmb * nnb * gridDim.z;
-  const int flat = blockIdx.x + nmb * (blockIdx.y + nnb * blockIdx.z);
-  const int xcd = flat & 7, slot = flat >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int nb = wid % nnb;
-  const int mb = (wid / nnb) % nmb;
-  const int zb = wid / (nnb * nmb);
-  int kt_begin = 0, kt_end = p.kc_tap ? p.kc_tap * p.kh * p.kw : (p.K + BK - 1) / BK;
-  if (p.ktiles_per_split > 0) {
-    kt_begin = zb * p.ktiles_per_split;
-    kt_end = min(kt_end, kt_begin + p.ktiles_per_split);
-  }
-  if (wave >= WM * WN)
-    x3_producer<BM, BN, MODE, CAT, TI, PRO>(p, smem, kt_begin, kt_end, wave - WM * WN, lane, mb,
-                                            nb);
-  else
-    x3_consumer<BM, BN, WM, WN, MODE>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb);
-}
 
 // --------------------------------------------------------------------- patch mode
 // 3x3 stride-1 FWD/DGRAD convs whose input has exactly 32 channels (one source): the whole K =
@@ -1287,63 +788,6 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad64_pc_kernel(GemmConvP
   }
 }
 
-// ------------------------------------------------------------------------ schedules
-struct Cfg { int bm, bn, tm, tn, occ; };
-// occ: resident blocks per CU (LDS 2 (BM+BN) 128 B of 160 KiB; registers). tm x tn: 32x32 MFMA
-// tiles per consumer wave.
-static const Cfg kCfg[] = {
-    {256, 32, 2, 1, 2},  {128, 64, 2, 1, 3},  {128, 96, 1, 3, 2},  {128, 128, 2, 2, 2},
-    {128, 160, 1, 5, 2}, {128, 192, 1, 6, 1}, {128, 224, 1, 7, 1}, {256, 64, 2, 2, 1},
-    {256, 128, 4, 2, 1}, {128, 256, 2, 4, 1},
-    // short-M / long-K launches (the encoder's 14x14 and 28x28 1x1 convs at batch 32: 147-294
-    // tiles of 128 x 64 leave most of the 256 CUs idle): 4x the workgroups, 4 resident per CU
-    {64, 64, 1, 1, 4},
-    // short-M launches with narrow-but-not-tiny N (N = 112..320 at M = 6272 / 25088): one
-    // workgroup covers 2-3x the columns of a 64 x 64 tile, so the A strip is staged once per
-    // 128 / 192 columns instead of once per 64
-    {64, 128, 1, 2, 3},  {64, 192, 1, 3, 2},
-};
-constexpr int kNumCfg = (int)(sizeof(kCfg) / sizeof(kCfg[0]));
-
-template <int MODE, int BM, int BN, int WM, int WN>
-static void launch_cfg(GemmConvParams& p, int splits, hipStream_t st) {
-  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
-  constexpr int T = (WM * WN + 4) * 64;
-  if constexpr (MODE == MODE_FWD) {
-    if (p.in_scale) {  // one source (x3_fwd_geom)
-      if (p.kc_tap) conv_x3_kernel<BM, BN, WM, WN, MODE, false, true, true><<<grid, T, 0, st>>>(p);
-      else conv_x3_kernel<BM, BN, WM, WN, MODE, false, false, true><<<grid, T, 0, st>>>(p);
-      return;
-    }
-  }
-  if (MODE == MODE_FWD && p.kc_tap) {
-    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true, true><<<grid, T, 0, st>>>(p);
-    else conv_x3_kernel<BM, BN, WM, WN, MODE, false, true><<<grid, T, 0, st>>>(p);
-  } else {
-    if (p.c2) conv_x3_kernel<BM, BN, WM, WN, MODE, true, false><<<grid, T, 0, st>>>(p);
-    else conv_x3_kernel<BM, BN, WM, WN, MODE, false, false><<<grid, T, 0, st>>>(p);
-  }
-}
-
-template <int MODE>
-static void launch(GemmConvParams& p, int splits, int cfg, hipStream_t st) {
-  switch (cfg) {
-    case 0: launch_cfg<MODE, 256, 32, 4, 1>(p, splits, st); break;
-    case 1: launch_cfg<MODE, 128, 64, 2, 2>(p, splits, st); break;
-    case 2: launch_cfg<MODE, 128, 96, 4, 1>(p, splits, st); break;
-    case 3: launch_cfg<MODE, 128, 128, 2, 2>(p, splits, st); break;
-    case 4: launch_cfg<MODE, 128, 160, 4, 1>(p, splits, st); break;
-    case 5: launch_cfg<MODE, 128, 192, 4, 1>(p, splits, st); break;
-    case 6: launch_cfg<MODE, 128, 224, 4, 1>(p, splits, st); break;
-    case 7: launch_cfg<MODE, 256, 64, 4, 1>(p, splits, st); break;
-    case 8: launch_cfg<MODE, 256, 128, 2, 2>(p, splits, st); break;
-    case 9: launch_cfg<MODE, 128, 256, 2, 2>(p, splits, st); break;
-    case 10: launch_cfg<MODE, 64, 64, 2, 2>(p, splits, st); break;
-    case 11: launch_cfg<MODE, 64, 128, 2, 2>(p, splits, st); break;
-    default: launch_cfg<MODE, 64, 192, 2, 2>(p, splits, st); break;
-  }
-}
-
 }  // namespace x3
 }  // namespace pld
 
@@ -1462,12 +906,26 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
   x3::conv_x3_patch_wgrad_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
   return check_launch("conv_x3_patch_wgrad_pc_kernel");
 }
-extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, void* stream) {
+// sk_grid > 0: the tile-stream schedule with that many workgroups (p->sk_* filled by the host;
+// non-aligned: p->sk_slab holds 2 sk_grid BM BN floats and the fixup kernel follows)
+extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, int sk_grid,
+                              void* stream) {
   if (mode == MODE_WGRAD && !pld__x3_wgrad_cfg_ok(cfg)) {
     set_error("conv_x3: schedule %d is not a WGRAD tile", cfg);
     return PLD_ERR_ARG;
   }
-  if (mode == MODE_FWD) x3::launch<MODE_FWD>(*p, splits, cfg, as_stream(stream));
-  else x3::launch<MODE_WGRAD>(*p, splits, cfg, as_stream(stream));
+  if (sk_grid > 0 && (p->in_scale || p->sk_nk <= 0 || p->sk_tiles <= 0 ||
+                      (!p->sk_align && !p->sk_slab))) {
+    set_error("conv_x3: bad tile-stream parameters");
+    return PLD_ERR_ARG;
+  }
+  hipStream_t st = as_stream(stream);
+  if (mode == MODE_FWD) {
+    if (sk_grid > 0) x3::launch_fwd_stream(*p, cfg, sk_grid, st);
+    else x3::launch_fwd_grid(*p, splits, cfg, st);
+  } else {
+    if (sk_grid > 0) x3::launch_wgrad_stream(*p, cfg, sk_grid, st);
+    else x3::launch_wgrad_grid(*p, splits, cfg, st);
+  }
   return check_launch("conv_x3_kernel");
 }

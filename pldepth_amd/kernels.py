@@ -362,8 +362,9 @@ def _patch_ok(mode, a):
 
 def _schedules(mode, math, a=None):
     """Schedule indices worth timing (pld_conv_args.tile): fwd/dgrad every tile x split-K
-    schedule (+ the patch kernel where it applies); wgrad sizes its own split, so only the tiles.
-    Under bf16x3 the exact-fp32 schedules follow the bf16x3 ones."""
+    schedule (+ the patch kernel where it applies, + the tile streams); wgrad sizes its own
+    split, so only the tiles (and tile streams). Under bf16x3 the exact-fp32 schedules follow
+    the bf16x3 ones. A call with an input prologue cannot stream (it would run the default)."""
     n = lib().pld_conv_num_schedules(math)
     out, patch_seen = [], False
     for i in range(n):
@@ -372,7 +373,9 @@ def _schedules(mode, math, a=None):
             if patch_seen:
                 continue
             patch_seen = True
-        if mode == "wgrad" and c not in (0, 2, 3):
+        if mode == "wgrad" and c not in (0, 2, 3, 5):
+            continue
+        if c == 5 and a is not None and a.in_scale:
             continue
         if c == 2 and (a is None or not _patch_ok(mode, a)):
             continue

@@ -16,7 +16,8 @@ Gradient bar (BASELINE.json: 1e-3 relative): per tensor 1e-3 wherever the fp32 r
 the reference semantics itself lands within 1e-3 of fp64, else 4x the fp32 restatement's own
 error (also for the measured ill-conditioned tensors of ILL_CONDITIONED); over all tensors
 together a global rel-L2 within max(1e-3, 2x the fp32 restatement's).
-The gradients of the reference semantics are themselves ill-conditioned at the 1e-3 level: training-mode BN cancels most of each incoming gradient, and
+The gradients of the reference semantics are themselves ill-conditioned at the 1e-3 level:
+training-mode BN cancels most of each incoming gradient, and
 an exact fp32 implementation lands ~1 % (median per tensor) from fp64 at batch 2 AND at the
 bench's batch 32 (ff_effnet 5 of 98 tensors within 1e-3, ff_redweb 3 of 237; profiles/r03_parity).
 bf16x3 products carry ~2^8 the rounding of fp32 ones; measured HIP / fp32-restatement error

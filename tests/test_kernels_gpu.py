@@ -270,6 +270,71 @@ def test_conv_every_schedule(cuda, case, math):
                                       torch.empty(n, h, w, cout, device=cuda).data_ptr(), 0, None)
 
 
+@pytest.mark.parametrize("case", [
+    # 1x1 on a 2 x 128 x 128 map: enough tiles to give workgroups several whole tiles (aligned
+    # ranges: the pipeline runs on across tile boundaries); its wgrad (K = 32768 pixels) cuts
+    # each tile over dozens of workgroups (fixup sums)
+    (2, 128, 128, 192, 0, 1, 160, True),
+    # dec_conv0-like 3x3 concat at 14 x 14 with long K (K = 11520): few tiles, stream-K cuts
+    (2, 14, 14, 640, 640, 3, 336, True),
+    # ragged everything: M, N and K tails, concat with a 16-channel chunk
+    (3, 11, 13, 48, 16, 3, 72, False)])
+def test_conv_tile_stream(cuda, case):
+    """The bf16x3 tile-stream schedules (conv_x3_kernel STREAM + x3_stream_fixup_kernel): fwd
+    (+bias, accumulate), dgrad into two concat destinations (accumulate on one), wgrad, and the
+    fused BN statistics of the forward (in the main kernel's epilogue for whole tiles, in the
+    fixup for cut ones) against fp64 / the unfused statistics pass."""
+    n, h, w, c1, c2, k, cout, has_bias = case
+    torch.manual_seed(11)
+    x1 = torch.randn(n, h, w, c1, dtype=torch.float64)
+    x2 = torch.randn(n, h, w, c2, dtype=torch.float64) if c2 else None
+    wt = torch.randn(k, k, c1 + c2, cout, dtype=torch.float64) / np.sqrt(k * k * (c1 + c2))
+    b = torch.randn(cout, dtype=torch.float64) if has_bias else None
+    pt, pb, _ = OE.same_pad(h, k, 1)
+    pl, pr, _ = OE.same_pad(w, k, 1)
+    x1r = x1.clone().requires_grad_(True)
+    x2r = x2.clone().requires_grad_(True) if x2 is not None else None
+    wr = wt.clone().requires_grad_(True)
+    y_ref = _ref_conv(x1r, x2r, wr, b, k, 1, pt, pb, pl, pr)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    gx1, gx2, gw = dev(x1, cuda), (dev(x2, cuda) if c2 else None), dev(wt, cuda)
+    wn, wd = K.filter_to_native(gw), K.filter_to_dgrad(gw)
+    gb, gdy = (dev(b, cuda) if has_bias else None), dev(dy, cuda)
+    lib = _lib.lib()
+    m = K.MATH["bf16x3"]
+    streams = [t for t in range(lib.pld_conv_num_schedules(m))
+               if lib.pld_conv_schedule_class(m, t) == 5]
+    assert streams and all(K.schedule_desc(m, t).startswith("x3stream/") for t in streams)
+    rows = n * h * w
+    for t in streams:
+        args = K.conv_args(gx1, gx2, k, k, 1, pt, pl, h, w, cout, math="bf16x3")
+        args.tile = t
+        assert K.conv_kernel_name(args, "fwd") == "conv_x3_kernel"
+        y = torch.full((n, h, w, cout), 0.5, device=cuda)
+        K.conv2d_fwd(args, wn, gb, y, accumulate=True)
+        dx1 = torch.empty_like(gx1)
+        dx2 = torch.full_like(gx2, 1.0) if c2 else None
+        K.conv2d_dgrad(args, gdy, wd, dx1, dx2, acc2=True)
+        dw = torch.empty(k, k, c1 + c2, cout, device=cuda)
+        K.conv2d_wgrad(args, gdy, dw)
+        y2 = torch.empty(n, h, w, cout, device=cuda)
+        mean, inv = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+        K.conv2d_fwd_bn_stats(args, wn, gb, y2, mean, inv)
+        torch.cuda.synchronize()
+        desc = K.schedule_desc(m, t)
+        assert rel_err(y - 0.5, y_ref) < 1e-4, (desc, rel_err(y - 0.5, y_ref))
+        assert torch.equal(y2, y - 0.5) or rel_err(y2, y_ref) < 1e-4, desc
+        assert rel_err(dx1, x1r.grad) < 1e-4, desc
+        if c2:
+            assert rel_err(dx2 - 1.0, x2r.grad) < 1e-4, desc
+        assert rel_err(dw, wr.grad) < 1e-4, (desc, rel_err(dw, wr.grad))
+        m_ref, i_ref = torch.empty(cout, device=cuda), torch.empty(cout, device=cuda)
+        K.bn_stats(y2, rows, cout, m_ref, i_ref)
+        torch.cuda.synchronize()
+        assert rel_err(mean, m_ref) < 1e-6 and rel_err(inv, i_ref) < 1e-6, desc
+
+
 @pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("case", [(2, 14, 12, 64, 3, 96, "relu"), (1, 9, 11, 256, 1, 64, "relu"),
                                   (2, 10, 9, 32, 3, 48, "swish"), (2, 7, 9, 128, 3, 130, "relu"),
