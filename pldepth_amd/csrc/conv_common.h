@@ -53,6 +53,14 @@ struct GemmConvParams {
 };
 
 // first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)
+// XCD-aware workgroup order: workgroups are dealt round-robin to the 8 XCDs (flat ids b, b + 8,
+// ... share one), so virtual id = the flat id's slot in a contiguous run per XCD. Bijective on
+// [0, nwg); neighbouring virtual ids (which share operands) meet in one XCD's L2.
+__device__ __forceinline__ int xcd_order(int flat, int nwg) {
+  const int xcd = flat & 7, slot = flat >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+}
+
 __host__ __device__ inline long sk_begin(const GemmConvParams& p, long w, long G) {
   return p.sk_align ? (w * p.sk_tiles / G) * p.sk_nk : w * ((long)p.sk_tiles * p.sk_nk) / G;
 }
@@ -91,6 +99,37 @@ __device__ __forceinline__ float4 prologue4(int act, float4 v, float4 s, float4 
                      act_fwd(act, v.z * s.z + t.z), act_fwd(act, v.w * s.w + t.w));
 }
 
+// the BN statistics partial of a wave's accumulators (store_acc's layout; p.stats set)
+template <int TM, int TN>
+__device__ __forceinline__ void acc_stats(const GemmConvParams& p, const floatx16 (&acc)[TM][TN],
+                                          int m_w, int n_w, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+  // per column: this wave's rows summed in fp64 (the lane's 16 x TM rows, then the other half
+  // wave's through a cross-half swap); lanes 0-31 own one column each. Written for every wave
+  // row tile (zeros past M), so the finalize reads stats_parts whole slots per channel.
+  const int part = m_w / (TM * 32);
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n_w + b * 32 + l32;
+    const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const double v = row < p.M ? (double)(acc[a][b][r] + bias) : 0.0;
+        s += v;
+        q += v * v;
+      }
+    s += __shfl_xor(s, 32);
+    q += __shfl_xor(q, 32);
+    if (h == 0 && col < p.N)
+      *reinterpret_cast<double2*>(p.stats + ((long)col * p.stats_parts + part) * 2) =
+          make_double2(s, q);
+  }
+}
+
 // ---- epilogue of a wave's TM x TN grid of 32x32 accumulators (C/D map of the 32x32 MFMA
 // forms: column = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)). m_w/n_w: the wave's first
 // output row/column. Split-K slabs (zstride > 0) get the raw sums; otherwise bias, two-way
@@ -115,32 +154,7 @@ __device__ __forceinline__ void store_acc(const GemmConvParams& p, const floatx1
       }
     return;
   }
-  if (p.stats) {
-    // per column: this wave's rows summed in fp64 (the lane's 16 x TM rows, then the other half
-    // wave's through a cross-half swap); lanes 0-31 own one column each. Written for every wave
-    // row tile (zeros past M), so the finalize reads stats_parts whole slots per channel.
-    const int part = m_w / (TM * 32);
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int col = n_w + b * 32 + l32;
-      const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
-      double s = 0.0, q = 0.0;
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m_w + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const double v = row < p.M ? (double)(acc[a][b][r] + bias) : 0.0;
-          s += v;
-          q += v * v;
-        }
-      s += __shfl_xor(s, 32);
-      q += __shfl_xor(q, 32);
-      if (h == 0 && col < p.N)
-        *reinterpret_cast<double2*>(p.stats + ((long)col * p.stats_parts + part) * 2) =
-            make_double2(s, q);
-    }
-  }
+  if (p.stats) acc_stats<TM, TN>(p, acc, m_w, n_w, lane);
   if (!p.acc1 && !p.acc2) {
 #pragma unroll
     for (int a = 0; a < TM; ++a)

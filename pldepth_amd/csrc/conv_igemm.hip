@@ -784,6 +784,10 @@ extern "C" size_t pld__scalar1x1_wgrad_ws(void);
 extern "C" int pld__scalar1x1_wgrad(const float* x, const float* dy, float* dw, long n,
                                     int accumulate, void* ws, void* stream);
 extern "C" int pld__skinny_eligible(const pld_conv_args* a);
+extern "C" int pld__stem3x3_eligible(const pld_conv_args* a);
+extern "C" int pld__stem3x3_parts(const pld_conv_args* a);
+extern "C" int pld__stem3x3_fwd(const pld_conv_args* a, const float* w_nat, const float* bias,
+                                float* y, int accumulate, double* stats, void* stream);
 extern "C" int pld__skinny_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,
                                float* y, int accumulate, void* stream);
 extern "C" int pld__skinny_dgrad(const pld_conv_args* a, const float* dy, const float* w_dgrad,
@@ -1181,6 +1185,8 @@ extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const
   int rc = fill_geom(a, p);
   if (rc) return rc;
   PLD_CHECK_ARG(w_ohwi && y, "pld_conv2d_fwd: null w/y");
+  if (pld__stem3x3_eligible(a) && aligned16(y))
+    return pld__stem3x3_fwd(a, w_ohwi, bias, y, accumulate, nullptr, stream);
   if (pld__scalar1x1_eligible(a) && aligned16(a->x1) && aligned16(y))
     return pld__scalar1x1_apply(a->x1, w_ohwi, bias, y, (long)a->n * a->h * a->w, accumulate,
                                 stream);
@@ -1233,7 +1239,9 @@ extern "C" size_t pld_conv2d_fwd_bn_stats_workspace_size(const pld_conv_args* a)
                           : 0;
   // GEMM epilogue partials: cdiv(M, BM) x BM / (32 TM) <= M / 32 + 8 per channel
   const size_t gemm = sizeof(double) * 2 * (size_t)a->cout * (cdiv(rows, 32) + 8);
-  return std::max(std::max(std::max(thin, wide), gemm),
+  const size_t stem =
+      pld__stem3x3_eligible(a) ? sizeof(double) * 2 * (size_t)a->cout * pld__stem3x3_parts(a) : 0;
+  return std::max(std::max(std::max(std::max(thin, wide), gemm), stem),
                   pld_channel_reduce_workspace_size(rows, a->cout));
 }
 
@@ -1248,6 +1256,13 @@ extern "C" int pld_conv2d_fwd_bn_stats(const pld_conv_args* a, const float* w_oh
   PLD_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr),
                 "pld_conv2d_fwd_bn_stats: moving_mean/moving_var must both be given or both NULL");
   const long rows = (long)a->n * a->oh * a->ow;
+  if (pld__stem3x3_eligible(a) && aligned16(y)) {
+    int rc = pld__stem3x3_fwd(a, w_ohwi, bias, y, 0, (double*)ws, stream);
+    if (rc) return rc;
+    return pld__bn_stats_finish((const double*)ws, pld__stem3x3_parts(a), rows, a->cout, eps,
+                                momentum, mean, invstd, moving_mean, moving_var,
+                                as_stream(stream));
+  }
   if (fwd_stats_thin(a, w_ohwi, y)) {
     int rc = pld__thin_gemm(a->x1, w_ohwi, bias, y, rows, a->c1, a->cout, 0, stream,
                             (double*)ws);
@@ -1327,6 +1342,7 @@ extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
 
 extern "C" int pld_conv_kernel_kind(const pld_conv_args* a, int mode) {
   if (!a || mode < 0 || mode > 2) return -1;
+  if (mode == 0 && pld__stem3x3_eligible(a)) return PLD_KIND_DIRECT;
   if (pld__scalar1x1_eligible(a)) return PLD_KIND_DIRECT;
   if (pld__skinny_eligible(a) && !(mode == 1 && (a->sh != 1 || a->sw != 1)))
     return PLD_KIND_DIRECT;
@@ -1355,6 +1371,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
   const int kind = pld_conv_kernel_kind(a, mode);
   if (kind < 0) return "";
   if (kind == PLD_KIND_DIRECT) {
+    if (mode == 0 && pld__stem3x3_eligible(a)) return "stem3x3_kernel";
     if (pld__scalar1x1_eligible(a))
       return mode == 2 ? "scalar1x1_wgrad_kernel" : "scalar1x1_kernel";
     if (pld__skinny_eligible(a))
@@ -1385,7 +1402,7 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
 
 extern "C" size_t pld_conv2d_fwd_workspace_size(const pld_conv_args* a) {
   if (!a || a->n <= 0 || a->c1 <= 0 || a->cout <= 0 || a->oh <= 0 || a->ow <= 0) return 0;
-  if (pld__skinny_eligible(a) || pld__scalar1x1_eligible(a)) return 0;
+  if (pld__skinny_eligible(a) || pld__scalar1x1_eligible(a) || pld__stem3x3_eligible(a)) return 0;
   return fwd_ws_bytes((long)a->n * a->oh * a->ow, a->cout,
                       (long)a->kh * a->kw * (a->c1 + a->c2), a->kh * a->kw, a->c1, a->c2, a->tile,
                       a->math,

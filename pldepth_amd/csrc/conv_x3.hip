@@ -411,7 +411,15 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad_pc_kernel(GemmConvPar
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PW_STAGE];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  // several cout tiles (N > 32): XCD-aware order, cout tile fastest, then chunk, then split —
+  // the workgroups an XCD runs at once share one tile range, so a chunk's patch is fetched once
+  // for its cout tiles and a dY tile once for the concurrent chunks (dec2 dW, N = 144: 873 ->
+  // 501 MB fetched per launch, time unchanged); one cout tile: launch order (dec3 dW measured 6 %
+  // slower with the XCD order, nothing to share across cout tiles)
+  const int flat = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int wid = gridDim.y > 1 ? xcd_order(flat, gridDim.x * gridDim.y * gridDim.z) : flat;
+  const int nb = wid % gridDim.y, q = (wid / gridDim.y) % gridDim.x,
+            zb = wid / (gridDim.x * gridDim.y);
   const bool s2 = q >= p.kc1;
   const int cb = (s2 ? q - p.kc1 : q) * 32;
   const int cs = s2 ? p.c2 : p.c1;
@@ -616,7 +624,11 @@ __global__ __launch_bounds__(512) void conv_x3_patch_wgrad64_pc_kernel(GemmConvP
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Q_STAGE];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x, nb = blockIdx.y, zb = blockIdx.z;
+  const int flat = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int wid = gridDim.y > 1 ? xcd_order(flat, gridDim.x * gridDim.y * gridDim.z)
+                                : flat;  // as the 32-wide kernel
+  const int nb = wid % gridDim.y, q = (wid / gridDim.y) % gridDim.x,
+            zb = wid / (gridDim.x * gridDim.y);
   const bool s2 = q >= p.kc1;
   const int cb = (s2 ? q - p.kc1 : q) * 32;
   const int cs = s2 ? p.c2 : p.c1;

@@ -1352,3 +1352,48 @@ def test_filter_refresh(cuda, kh, cin, cout):
     if ds is not None:
         assert torch.equal(ds, K.filter_split(dg_ref))
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,h,w,pt,pl", [(2, 64, 64, 0, 0), (1, 37, 51, 1, 1), (3, 18, 70, 0, 1),
+                                          (1, 448, 448, 0, 0)])
+def test_stem3x3(cuda, n, h, w, pt, pl):
+    """The direct EfficientNet stem kernel (stem.hip: 3x3 stride 2, 3 -> 32, the Rescaling /
+    Normalization prologue on in-image taps, correct_pad's asymmetric zero padding) against
+    fp64: plain, +bias, +accumulate, and its epilogue BN statistics against pld_bn_stats of the
+    stored output. Ragged 8 x 32 output tiles at the right and bottom edges."""
+    g = torch.Generator(device=cuda).manual_seed(h * w + pt)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    x = torch.rand(n, h, w, 3, device=cuda, generator=g)
+    wt = torch.randn(3, 3, 3, 32, device=cuda, generator=g) / 27 ** 0.5
+    b = torch.randn(32, device=cuda, generator=g)
+    sc = torch.tensor([1 / 0.229, 1 / 0.224, 1 / 0.225], device=cuda)
+    sh = torch.tensor([-0.485 / 0.229, -0.456 / 0.224, -0.406 / 0.225], device=cuda)
+    wn = K.filter_to_native(wt)
+    args = K.conv_args(x, None, 3, 3, 2, pt, pl, oh, ow, 32, in_scale=sc, in_shift=sh,
+                       math="bf16x3")
+    assert K.conv_kernel_name(args, "fwd") == "stem3x3_kernel"
+    xd = x.double() * sc.double() + sh.double()
+    pb = max(0, (oh - 1) * 2 + 3 - h - pt)
+    pr = max(0, (ow - 1) * 2 + 3 - w - pl)
+    xp = torch.nn.functional.pad(xd.permute(0, 3, 1, 2), (pl, pr, pt, pb))
+    ref = torch.nn.functional.conv2d(xp, wt.double().permute(3, 2, 0, 1), stride=2)
+    ref = ref.permute(0, 2, 3, 1)[:, :oh, :ow]
+    y = torch.empty(n, oh, ow, 32, device=cuda)
+    K.conv2d_fwd(args, wn, None, y)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 1e-6, rel_err(y, ref)
+    K.conv2d_fwd(args, wn, b, y, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, 2 * ref + b.double()) < 1e-6
+    rows = n * oh * ow
+    y2 = torch.empty_like(y)
+    m, i = torch.empty(32, device=cuda), torch.empty(32, device=cuda)
+    mm, mv = torch.zeros(32, device=cuda), torch.ones(32, device=cuda)
+    K.conv2d_fwd_bn_stats(args, wn, b, y2, m, i, mm, mv)
+    m_ref, i_ref = torch.empty(32, device=cuda), torch.empty(32, device=cuda)
+    mm_ref, mv_ref = torch.zeros(32, device=cuda), torch.ones(32, device=cuda)
+    K.bn_stats(y2, rows, 32, m_ref, i_ref, mm_ref, mv_ref)
+    torch.cuda.synchronize()
+    assert rel_err(y2, ref + b.double()) < 1e-6
+    for a, r in ((m, m_ref), (i, i_ref), (mm, mm_ref), (mv, mv_ref)):
+        assert rel_err(a, r) < 1e-6, rel_err(a, r)

@@ -54,6 +54,19 @@ def main():
         "source": pmc, "bench_line": bench_file,
         "note": "FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes, one eager step",
     }
+    mdir = os.path.join(pmc, "mfma")
+    if os.path.isdir(mdir):
+        # MFMA busy share: SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over the 1024 SIMDs) over the
+        # launches' own cycles (GRBM_GUI_ACTIVE, summed over the 8 XCDs: / 8), same launches
+        mb = T.window(T.load(mdir, "SQ_VALU_MFMA_BUSY_CYCLES"), "adam_amsgrad_dev_kernel")
+        gr = T.window(T.load(mdir, "GRBM_GUI_ACTIVE"), "adam_amsgrad_dev_kernel")
+        busy = cyc = 0.0
+        for (_, n1, v1, _), (_, n2, v2, _) in zip(mb, gr):
+            if short(n1.split("::")[-1]) == kname or short(n1) == kname:
+                busy += v1
+                cyc += v2 / 8
+        if cyc > 0:
+            res["mfma_busy"] = round(busy / (1024 * cyc), 4)
     with open(out + ".json", "w") as fh:
         json.dump(res, fh, indent=1)
     with open(out + ".txt", "w") as fh:
@@ -63,6 +76,8 @@ def main():
         fh.write(f"HBM per launch: {res['hbm_bytes_per_launch'] / 1e6:.2f} MB; algorithmic per "
                  f"launch: {res['algorithmic_bytes_per_launch'] / 1e6:.2f} MB; ratio "
                  f"{res['hbm_over_algorithmic']}\n")
+        if "mfma_busy" in res:
+            fh.write(f"MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles): {res['mfma_busy']}\n")
         fh.write(f"{'read MB':>9} {'write MB':>9} {'us':>8}  launch\n")
         for name, r_, w_, d in rows:
             fh.write(f"{r_ / 1e6:9.2f} {w_ / 1e6:9.2f} {d / 1e3:8.1f}  {name[:110]}\n")

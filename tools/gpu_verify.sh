@@ -8,12 +8,15 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+TEST_RC=0
 if [ "$2" != "--no-tests" ]; then
   export PLD_REPORT_DIR=$O/parity
   timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
-  rc=$?
+  TEST_RC=$?
   tail -3 $O/gputest.log
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  # a test failure (1) still lets the bench / trace run; anything else (a crash, a time limit)
+  # ends the call; either way the script's exit status reports it
+  if [ $TEST_RC -ne 0 ] && [ $TEST_RC -ne 1 ]; then exit $TEST_RC; fi
 fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || exit 1
@@ -25,3 +28,4 @@ python3 $R/tools/kstats.py $DB --marker adam_amsgrad_dev_kernel --steps 10 --ski
 rm -rf $O/trace
 head -3 $O/kstats.txt
 echo done
+exit $TEST_RC

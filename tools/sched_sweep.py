@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def sweep(mode, n, h, w, c1, c2, k, cout, math="bf16x3", reps=10, replays=5, scheds=None):
+def sweep(mode, n, h, w, c1, c2, k, cout, math="bf16x3", reps=10, replays=5, scheds=None,
+          stride=1, pad=None):
     from pldepth_amd import kernels as K
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -23,24 +24,25 @@ def sweep(mode, n, h, w, c1, c2, k, cout, math="bf16x3", reps=10, replays=5, sch
     x2 = torch.randn(n, h, w, c2, device=dev, generator=g) if c2 else None
     C = c1 + c2
     wt = torch.randn(k, k, C, cout, device=dev, generator=g) / (k * k * C) ** 0.5
-    pt = (k - 1) // 2
+    pt = (k - 1) // 2 if pad is None else pad
+    oh, ow = (h - 1) // stride + 1, (w - 1) // stride + 1
     wn, wd = K.filter_to_native(wt), K.filter_to_dgrad(wt)
     if math == "bf16x3":
         if C % 8 == 0:
             K.filter_split(wn, torch.empty_like(wn))
         if cout % 8 == 0:
             K.filter_split(wd, torch.empty_like(wd))
-    y = torch.empty(n, h, w, cout, device=dev)
+    y = torch.empty(n, oh, ow, cout, device=dev)
     dy = torch.randn_like(y)
     dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if x2 is not None else None)
     dw = torch.empty_like(wt)
-    base = K.conv_args(x1, x2, k, k, 1, pt, pt, h, w, cout, math=math)
-    fl = 2.0 * n * h * w * cout * k * k * C
-    by = 4.0 * (n * h * w * C + n * h * w * cout + k * k * C * cout)
+    base = K.conv_args(x1, x2, k, k, stride, pt, pt, oh, ow, cout, math=math)
+    fl = 2.0 * n * oh * ow * cout * k * k * C
+    by = 4.0 * (n * h * w * C + n * oh * ow * cout + k * k * C * cout)
     out = []
     st = torch.cuda.Stream()
     for t in (scheds if scheds is not None else K._schedules(mode, base.math, base)):
-        args = K.conv_args(x1, x2, k, k, 1, pt, pt, h, w, cout, math=math)
+        args = K.conv_args(x1, x2, k, k, stride, pt, pt, oh, ow, cout, math=math)
         args.tile = t
         run = {"fwd": lambda: K.conv2d_fwd(args, wn, None, y),
                "dgrad": lambda: K.conv2d_dgrad(args, dy, wd, dx1, dx2),
@@ -75,13 +77,15 @@ def main():
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cout", type=int, default=1152)
     ap.add_argument("--math", default="bf16x3")
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--pad", type=int, default=None, help="top/left padding (default (k-1)/2)")
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--sched", type=int, nargs="*", default=None,
                     help="only these schedule indices (e.g. for a rocprofv3 counter pass)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     res, fl, by = sweep(a.mode, a.n, a.h, a.w, a.c1, a.c2, a.k, a.cout, a.math,
-                        scheds=a.sched)
+                        scheds=a.sched, stride=a.stride, pad=a.pad)
     print(f"{a.mode} n{a.n} {a.h}x{a.w} c{a.c1}+{a.c2} k{a.k} cout{a.cout} {a.math}: "
           f"{fl / 1e9:.2f} GFLOP, {by / 1e6:.1f} MB algorithmic")
     for us, t, desc, kname in res[:a.top]:
