@@ -482,6 +482,50 @@ def test_bn_forward_backward(cuda, rows, c, act):
     assert rel_err(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("rows,c", [(401408, 24), (6272, 1152), (777, 40)])
+def test_bn_in_kernel_finalize_repeats(cuda, rows, c):
+    """The reductions finalize inside chan_reduce_kernel (two levels of last-arriving
+    workgroups on self-resetting tickets): repeated eager launches and replays of a captured
+    graph give bit-identical statistics, coefficients and gradients (the tickets are back at
+    zero after every launch; the summation order does not depend on who arrives last)."""
+    g = torch.Generator(device=cuda).manual_seed(rows + c)
+    x = torch.randn(rows, c, device=cuda, generator=g) * 2 + 0.5
+    dy = torch.randn(rows, c, device=cuda, generator=g)
+    gamma = torch.rand(c, device=cuda, generator=g) + 0.5
+    beta = torch.randn(c, device=cuda, generator=g)
+    outs = [torch.empty(c, device=cuda) for _ in range(4)] + [torch.empty_like(x)] + \
+        [torch.empty(c, device=cuda)]
+    gm, gi, dg, db, dx, cs = outs
+
+    def run():
+        K.bn_stats(x, rows, c, gm, gi)
+        K.bn_bwd(x, dy, rows, c, gm, gi, gamma, beta, "swish", dx, dg, db)
+        K.channel_sum(dy, rows, c, cs)
+
+    run()
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in outs]
+    x64, dy64 = x.double(), dy.double()
+    assert rel_err(gm, x64.mean(0)) < 1e-6
+    assert rel_err(cs, dy64.sum(0)) < 1e-5
+    for _ in range(2):
+        for t in outs:
+            t.fill_(float("nan"))
+        run()
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(outs, ref))
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        gr = K.Graph().capture(run)
+        for _ in range(3):
+            for t in outs:
+                t.fill_(float("nan"))
+            gr.launch()
+            st.synchronize()
+            assert all(torch.equal(a, b) for a, b in zip(outs, ref))
+    del gr
+
+
 def test_bn_with_se_gate_and_addn(cuda):
     n, hw, c = 3, 50, 16
     rows = n * hw
