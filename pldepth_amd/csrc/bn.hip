@@ -37,75 +37,7 @@ struct RedParams {
   FastDiv dHW;
   double* partial;  // [C][gridDim.x][2]
   float* dz_out;    // BNBWD without gate/addn: also store dz = d(act input) (or NULL)
-  // In-kernel finalize (cnt != NULL): the workgroups of a channel group form sets of `set`; the
-  // last of each set to finish (ticket cnt[y][set]) sums the set's partials into part2
-  // ([C][nsets][2]), and the last set-summer (ticket cnt[y][nsets]) sums those and writes the
-  // result below — no finalize launch. Fixed summation order whoever arrives last
-  // (deterministic); tickets reset themselves for the next launch.
-  unsigned* cnt;
-  double* part2;
-  int set, nsets;
-  // finalize outputs: STATS -> mean/invstd (+ moving averages); SUM -> sum_out; BNBWD -> dbeta,
-  // dgamma, k12 = [mean dz | mean dz xhat]
-  float eps, momentum;
-  float *mean_out, *invstd_out, *mmean, *mvar;
-  float* sum_out;
-  int sum_acc;
-  float *dgamma, *dbeta, *k12;
-  int pacc;
 };
-
-// write-through (sc1) 8-byte stores / loads of the partials a last arriver on another XCD reads
-// (an agent-scope relaxed atomic access is a plain global_store / global_load with sc1: no fence)
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __longlong_as_double(__hip_atomic_load(
-      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED,
-      __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// the finalize arithmetic of one channel from its fp64 (sum, sum of squares | sum dz, sum dz xhat)
-template <int OP>
-__device__ __forceinline__ void finalize_channel(const RedParams& p, int c, double s, double q) {
-  if (OP == 0) {  // RED_STATS
-    const double n = (double)p.rows;
-    const double mu = s / n;
-    double var = q / n - mu * mu;
-    if (var < 0.0) var = 0.0;
-    p.mean_out[c] = (float)mu;
-    p.invstd_out[c] = (float)(1.0 / sqrt(var + (double)p.eps));
-    if (p.mmean) {
-      const double uvar = p.rows > 1 ? var * n / (n - 1.0) : var;
-      p.mmean[c] = p.mmean[c] - (p.mmean[c] - (float)mu) * (1.0f - p.momentum);
-      p.mvar[c] = p.mvar[c] - (p.mvar[c] - (float)uvar) * (1.0f - p.momentum);
-    }
-  } else if (OP == 1) {  // RED_SUM
-    p.sum_out[c] = p.sum_acc ? p.sum_out[c] + (float)s : (float)s;
-  } else {  // RED_BNBWD
-    if (p.dbeta) p.dbeta[c] = p.pacc ? p.dbeta[c] + (float)s : (float)s;
-    if (p.dgamma) p.dgamma[c] = p.pacc ? p.dgamma[c] + (float)q : (float)q;
-    p.k12[c] = (float)(s / (double)p.rows);
-    p.k12[p.C + c] = (float)(q / (double)p.rows);
-  }
-}
-
-// one ticket per workgroup on `c` (after every wave drained its write-through stores); true in
-// the last of `n` arrivals, which also resets the ticket. `flag`: LDS broadcast slot.
-__device__ __forceinline__ bool last_arrival(unsigned* c, unsigned n, double* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = t == n - 1;
-    if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last ? 1.0 : 0.0;
-  }
-  __syncthreads();
-  return *flag != 0.0;
-}
 
 template <int VW>
 __device__ __forceinline__ void ld(const float* p, float (&v)[VW]) {
@@ -125,8 +57,11 @@ __device__ __forceinline__ void st(float* p, const float (&v)[VW]) {
     *p = v[0];
 }
 
-template <int OP, int VW>
+// ACT >= 0: the BN backward's activation as a compile-time constant (no per-element switch on
+// p.act in the loop); -1: read p.act (the statistics / sum reductions do not use it)
+template <int OP, int VW, int ACT = -1>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
+  const int act_id = ACT >= 0 ? ACT : p.act;
   __shared__ double red[256][2 * VW];
   const int CV = p.C / VW;
   const int cbase = blockIdx.y * 256;
@@ -191,7 +126,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
           for (int u = 0; u < VW; ++u) {
             const float xh = (xv[j][u] - mean[u]) * inv[u];
             const float z = (xh * gam[u] + bet[u]) + rv[j][u];
-            const float dz = dv[j][u] * act_grad(p.act, z);
+            const float dz = dv[j][u] * act_grad(act_id, z);
             dzv[u] = dz;
             s0[u] += (double)dz;
             s1[u] += (double)dz * (double)xh;
@@ -231,7 +166,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         for (int u = 0; u < VW; ++u) {
           const float xh = (xv[u] - mean[u]) * inv[u];
           const float z = (xh * gam[u] + bet[u]) + rv[u];
-          const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
+          const float dz = (dv[u] * g[u] + a[u]) * act_grad(act_id, z);
           dzv[u] = dz;
           s0[u] += (double)dz;
           s1[u] += (double)dz * (double)xh;
@@ -254,58 +189,11 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         s1[u] += red[tid + j * ncv][VW + u];
       }
     }
-    // channel-major partials: the finalize's per-channel read is one contiguous run
+    // channel-major partials: the finalize kernel's per-channel read is one contiguous run
 #pragma unroll
-    for (int u = 0; u < VW; ++u) {
-      double* d = p.partial + (((long)(cv * VW + u)) * gridDim.x + blockIdx.x) * 2;
-      st_wt(d, s0[u]);
-      st_wt(d + 1, s1[u]);
-    }
-  }
-  if (!p.cnt) return;
-  // ---- in-kernel finalize: level 1, the last workgroup of this set sums the set's partials
-  const int set = blockIdx.x / p.set, s_lo = set * p.set,
-            s_hi = min((int)gridDim.x, s_lo + p.set);
-  unsigned* cnt = p.cnt + (long)blockIdx.y * (p.nsets + 1);
-  double* flag = &red[0][0];
-  __syncthreads();  // red's partial sums above are consumed
-  if (!last_arrival(cnt + set, (unsigned)(s_hi - s_lo), flag)) return;
-  const int ch0 = cbase * VW, nch = ncv * VW;
-  for (int k = tid; k < nch; k += 256) {
-    const double* run = p.partial + (long)(ch0 + k) * gridDim.x * 2;
-    double a = 0.0, b = 0.0;
-    int j = s_lo;
-    for (; j + 3 < s_hi; j += 4) {  // 4 partials in flight, summed in order
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[2 * u] = ld_wt(run + 2 * (j + u));
-        v[2 * u + 1] = ld_wt(run + 2 * (j + u) + 1);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a += v[2 * u];
-        b += v[2 * u + 1];
-      }
-    }
-    for (; j < s_hi; ++j) {
-      a += ld_wt(run + 2 * j);
-      b += ld_wt(run + 2 * j + 1);
-    }
-    double* d = p.part2 + ((long)(ch0 + k) * p.nsets + set) * 2;
-    st_wt(d, a);
-    st_wt(d + 1, b);
-  }
-  // ---- level 2: the last set-summer of this channel group sums the sets and finalizes
-  if (!last_arrival(cnt + p.nsets, (unsigned)p.nsets, flag)) return;
-  for (int k = tid; k < nch; k += 256) {
-    const double* run = p.part2 + (long)(ch0 + k) * p.nsets * 2;
-    double a = 0.0, b = 0.0;
-    for (int j = 0; j < p.nsets; ++j) {
-      a += ld_wt(run + 2 * j);
-      b += ld_wt(run + 2 * j + 1);
-    }
-    finalize_channel<OP>(p, ch0 + k, a, b);
+    for (int u = 0; u < VW; ++u)
+      *reinterpret_cast<double2*>(p.partial + (((long)(cv * VW + u)) * gridDim.x + blockIdx.x) * 2) =
+          make_double2(s0[u], s1[u]);
   }
 }
 
@@ -317,66 +205,26 @@ static void red_plan(long rows, int C, int& nbx, int& rpb) {
   nbx = (int)((rows + rpb - 1) / rpb);
 }
 
-// the in-kernel finalize's set size for nbx workgroups per channel group: ~sqrt(nbx) partials
-// summed by each set's last arriver, ~sqrt(nbx) set sums by the final one
-static void fin_plan(int nbx, int& set, int& nsets) {
-  set = 1;
-  while (set * set < nbx) ++set;
-  nsets = (nbx + set - 1) / set;
-}
-
-// self-resetting tickets of the in-kernel finalize: a library-owned pool zeroed once, handed out
-// in consecutive slices (a captured graph keeps its slices; every launch leaves them at zero, so
-// replays and later launches start clean; the ring is far longer than what can run at once).
-// Allocated on the first call, which must not be inside a stream capture (the engines' eager
-// warm-up step comes first); NULL there, and the caller launches the finalize kernel instead.
-static unsigned* ticket_slots(long n, hipStream_t st) {
-  constexpr long kPool = 1L << 20;
-  static unsigned* pool = nullptr;
-  static long next = 0;
-  if (!pool) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-      return nullptr;
-    unsigned* q = nullptr;
-    if (hipMalloc(&q, kPool * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(q, 0, kPool * sizeof(unsigned)) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(q);
-      return nullptr;
-    }
-    pool = q;
-  }
-  if (n > kPool) return nullptr;
-  if (next + n > kPool) next = 0;
-  unsigned* r = pool + next;
-  next += n;
-  return r;
-}
-
-// part2: the level-2 partial area ([C][nsets][2] doubles), or NULL for no in-kernel finalize.
-// *finalized: whether the launch finalizes itself (else the caller launches the finalize).
-static int launch_reduce(int op, RedParams& p, hipStream_t st, double* part2 = nullptr,
-                         bool* finalized = nullptr) {
+static int launch_reduce(int op, RedParams& p, hipStream_t st) {
   int nbx, rpb;
   red_plan(p.rows, p.C, nbx, rpb);
   p.rows_per_block = rpb;
   const bool v4 = (p.C % 4 == 0);
   const int CV = p.C / (v4 ? 4 : 1);
   dim3 grid(nbx, cdiv(CV, 256));
-  p.cnt = nullptr;
-  if (part2) {
-    fin_plan(nbx, p.set, p.nsets);
-    p.part2 = part2;
-    p.cnt = ticket_slots((long)grid.y * (p.nsets + 1), st);
-  }
-  if (finalized) *finalized = p.cnt != nullptr;
 #define PLD_RED(OPV)                                                                         \
   if (v4) chan_reduce_kernel<OPV, 4><<<grid, 256, 0, st>>>(p);                               \
   else chan_reduce_kernel<OPV, 1><<<grid, 256, 0, st>>>(p);
+#define PLD_RED_ACT(A)                                                                       \
+  if (v4) chan_reduce_kernel<RED_BNBWD, 4, A><<<grid, 256, 0, st>>>(p);                      \
+  else chan_reduce_kernel<RED_BNBWD, 1, A><<<grid, 256, 0, st>>>(p);
   if (op == RED_STATS) { PLD_RED(RED_STATS) }
   else if (op == RED_SUM) { PLD_RED(RED_SUM) }
+  else if (p.act == ACT_NONE) { PLD_RED_ACT(ACT_NONE) }
+  else if (p.act == ACT_RELU) { PLD_RED_ACT(ACT_RELU) }
+  else if (p.act == ACT_SWISH) { PLD_RED_ACT(ACT_SWISH) }
   else { PLD_RED(RED_BNBWD) }
+#undef PLD_RED_ACT
 #undef PLD_RED
   return check_launch("chan_reduce_kernel");
 }
@@ -531,23 +379,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
     }
 #pragma unroll
     for (int u = 0; u < VW; ++u) xv[u] = act_fwd(p.act, xv[u]) * g[u];
-#if defined(PLD_EXP_STORE) && PLD_EXP_STORE > 0  // timing experiment: store cache policy
-    if constexpr (VW == 4) {
-      typedef unsigned u32x4e __attribute__((ext_vector_type(4)));
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          p.y, (short)0, (int)min(p.rows * p.C * 4, 0x7FFFFFF0L), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(u32x4e, make_float4(xv[0], xv[1], xv[2], xv[3])), rs,
-          (unsigned)(e * 16), 0, PLD_EXP_STORE == 1 ? 16 : 2);
-    } else {
-      p.y[e] = xv[0];
-    }
-#else
     if constexpr (VW == 4)
-      *reinterpret_cast<float4*>(p.y + e * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+      st_nt4(p.y + e * 4, make_float4(xv[0], xv[1], xv[2], xv[3]));
     else
       p.y[e] = xv[0];
-#endif
   }
 }
 
@@ -573,8 +408,9 @@ struct BwdApplyParams {
   int dres_acc;
 };
 
-template <int VW>
+template <int VW, int ACT = -1>  // ACT >= 0: compile-time activation (as chan_reduce_kernel)
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
+  const int act_id = ACT >= 0 ? ACT : p.act;
   const long nv = p.rows * p.C / VW;
   const int CV = p.C / VW;
   long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -609,7 +445,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
     for (int u = 0; u < VW; ++u) {
       const float xh = (xv[u] - mu[u]) * is[u];
       const float z = (xh * ga[u] + be[u]) + rv[u];
-      const float dz = (dv[u] * g[u] + a[u]) * act_grad(p.act, z);
+      const float dz = (dv[u] * g[u] + a[u]) * act_grad(act_id, z);
       dzs[u] = dz;
       o[u] = (is[u] * ga[u]) * (dz - k1[u] - xh * k2[u]);
     }
@@ -628,7 +464,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
         const float4 old = *d;
         v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
       }
-      *d = v;
+      st_nt4(reinterpret_cast<float*>(d), v);
     } else {
       p.dx[e] = p.acc ? p.dx[e] + o[0] : o[0];
     }
@@ -651,21 +487,6 @@ static size_t red_ws_doubles(long rows, int C) {
   int nbx, rpb;
   red_plan(rows, C, nbx, rpb);
   return (size_t)nbx * C * 2;
-}
-
-// workspace layout: [partials: red_ws_doubles][k12: 2C floats][level-2 partials: C nsets 2]
-static size_t k12_offset(long rows, int C) { return red_ws_doubles(rows, C) * sizeof(double); }
-static size_t part2_offset(long rows, int C) {
-  return (k12_offset(rows, C) + 2 * sizeof(float) * (size_t)C + 15) / 16 * 16;
-}
-static size_t part2_bytes(long rows, int C) {
-  int nbx, rpb, set, nsets;
-  red_plan(rows, C, nbx, rpb);
-  fin_plan(nbx, set, nsets);
-  return sizeof(double) * 2 * (size_t)C * nsets;
-}
-static double* part2_of(void* ws, long rows, int C) {
-  return reinterpret_cast<double*>((char*)ws + part2_offset(rows, C));
 }
 
 __global__ void bn_infer_kernel(const float* __restrict__ g, const float* __restrict__ b,
@@ -751,9 +572,8 @@ extern "C" int pld_bn_inference_coeffs(const float* gamma, const float* beta,
 
 extern "C" size_t pld_channel_reduce_workspace_size(int64_t rows, int c) {
   if (rows <= 0 || c <= 0) return 0;
-  // fp64 partials + 2*C floats of BN-backward coefficients + the in-kernel finalize's level-2
-  // partials
-  return part2_offset(rows, c) + part2_bytes(rows, c) + 64;
+  // fp64 partials + 2*C floats of BN-backward coefficients
+  return red_ws_doubles(rows, c) * sizeof(double) + 2 * sizeof(float) * (size_t)c + 64;
 }
 
 extern "C" int pld_channel_sum(const float* x, int64_t rows, int c, float* out, int accumulate,
@@ -765,12 +585,9 @@ extern "C" int pld_channel_sum(const float* x, int64_t rows, int c, float* out, 
   p.rows = rows;
   p.C = c;
   p.partial = (double*)ws;
-  p.sum_out = out;
-  p.sum_acc = accumulate;
   hipStream_t st = as_stream(stream);
-  bool fin = false;
-  int rc = launch_reduce(RED_SUM, p, st, part2_of(ws, rows, c), &fin);
-  if (rc || fin) return rc;
+  int rc = launch_reduce(RED_SUM, p, st);
+  if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
   sum_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, out, accumulate);
@@ -789,16 +606,9 @@ extern "C" int pld_bn_stats(const float* x, int64_t rows, int c, float eps, floa
   p.rows = rows;
   p.C = c;
   p.partial = (double*)ws;
-  p.eps = eps;
-  p.momentum = momentum;
-  p.mean_out = mean;
-  p.invstd_out = invstd;
-  p.mmean = moving_mean;
-  p.mvar = moving_var;
   hipStream_t st = as_stream(stream);
-  bool fin = false;
-  int rc = launch_reduce(RED_STATS, p, st, part2_of(ws, rows, c), &fin);
-  if (rc || fin) return rc;
+  int rc = launch_reduce(RED_STATS, p, st);
+  if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
   stats_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, eps, momentum,
@@ -889,8 +699,7 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
                          const float* gamma, const float* beta, int act, const float* gate,
                          const float* addn, FastDiv dHW, const float* res, float* dx,
                          int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
-                         float* dbeta, int param_accumulate, float* k12, hipStream_t st,
-                         bool finalized = false);
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st);
 
 static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, const float* mean,
                        const float* invstd, const float* gamma, const float* beta, int act,
@@ -926,23 +735,18 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
                        dres != dy && dres != x && dres != res;
   if (res && act == ACT_NONE) p.res = nullptr;
   if (dz_pass) p.dz_out = dres;
-  float* k12 = reinterpret_cast<float*>((char*)ws + k12_offset(rows, c));
-  p.dgamma = dgamma;
-  p.dbeta = dbeta;
-  p.pacc = param_accumulate;
-  p.k12 = k12;
-  bool fin = false;
-  int rc = launch_reduce(RED_BNBWD, p, st, part2_of(ws, rows, c), &fin);
+  int rc = launch_reduce(RED_BNBWD, p, st);
   if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
+  float* k12 = reinterpret_cast<float*>((char*)ws + red_ws_doubles(rows, c) * sizeof(double));
   if (dz_pass)
     return bn_bwd_finish(p.partial, nbx, x, dres, rows, c, mean, invstd, gamma, beta, ACT_NONE,
                          nullptr, nullptr, p.dHW, nullptr, dx, dx_accumulate, nullptr, 0, dgamma,
-                         dbeta, param_accumulate, k12, st, fin);
+                         dbeta, param_accumulate, k12, st);
   return bn_bwd_finish(p.partial, nbx, x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn,
                        p.dHW, p.res, dx, dx_accumulate, dres, dres_accumulate, dgamma, dbeta,
-                       param_accumulate, k12, st, fin);
+                       param_accumulate, k12, st);
 }
 
 // finalize (dgamma, dbeta, k1 = mean dz, k2 = mean dz xhat from nbx channel-major partials) +
@@ -952,15 +756,11 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
                          const float* gamma, const float* beta, int act, const float* gate,
                          const float* addn, FastDiv dHW, const float* res, float* dx,
                          int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
-                         float* dbeta, int param_accumulate, float* k12, hipStream_t st,
-                         bool finalized) {
-  if (!finalized) {
-    bnbwd_finalize_kernel<<<c, 256, 0, st>>>(part, nbx, c, rows, dgamma, dbeta,
-                                             param_accumulate, k12);
-    int rc = check_launch("bnbwd_finalize_kernel");
-    if (rc) return rc;
-  }
-  if (!(dx || dres)) return PLD_OK;
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st) {
+  bnbwd_finalize_kernel<<<c, 256, 0, st>>>(part, nbx, c, rows, dgamma, dbeta,
+                                                       param_accumulate, k12);
+  int rc = check_launch("bnbwd_finalize_kernel");
+  if (rc || !(dx || dres)) return rc;
   BwdApplyParams q{};
   q.x = x;
   q.dy = dy;
@@ -982,7 +782,11 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
   q.dres = dres;
   q.dres_acc = dres_accumulate;
   if (c % 4 == 0) {
-    bn_bwd_apply_kernel<4><<<ew_grid_c(rows * c / 4, c / 4), 256, 0, st>>>(q);
+    const unsigned g = ew_grid_c(rows * c / 4, c / 4);
+    if (act == ACT_NONE) bn_bwd_apply_kernel<4, ACT_NONE><<<g, 256, 0, st>>>(q);
+    else if (act == ACT_RELU) bn_bwd_apply_kernel<4, ACT_RELU><<<g, 256, 0, st>>>(q);
+    else if (act == ACT_SWISH) bn_bwd_apply_kernel<4, ACT_SWISH><<<g, 256, 0, st>>>(q);
+    else bn_bwd_apply_kernel<4><<<g, 256, 0, st>>>(q);
   } else {
     bn_bwd_apply_kernel<1><<<ew_grid_c(rows * c, c), 256, 0, st>>>(q);
   }
@@ -1028,13 +832,8 @@ extern "C" int pld_bn_bwd_coeffs(const float* x, const float* dy, int64_t rows, 
   p.act = act;
   p.dHW = FastDiv(1);
   p.partial = (double*)ws;
-  p.dgamma = dgamma;
-  p.dbeta = dbeta;
-  p.pacc = param_accumulate;
-  p.k12 = k12;
-  bool fin = false;
-  int rc = launch_reduce(RED_BNBWD, p, st, part2_of(ws, rows, c), &fin);
-  if (rc || fin) return rc;
+  int rc = launch_reduce(RED_BNBWD, p, st);
+  if (rc) return rc;
   int nbx, rpb;
   red_plan(rows, c, nbx, rpb);
   bnbwd_finalize_kernel<<<c, 256, 0, st>>>(p.partial, nbx, c, rows, dgamma, dbeta,

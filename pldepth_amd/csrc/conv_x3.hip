@@ -395,25 +395,19 @@ __device__ __forceinline__ bf16x8 tr_frag_rows(const unsigned char* plane, int r
 
 // Warp-specialised (round 3; a uniform-role form, where every wave holds 9 accumulator tiles +
 // the next tile's loads, left the matrix pipes idle while all waves split and stored: MFMA 31 %
-// busy). Consumer waves only compute — a wave owns output rows 2 rp, 2 rp + 1 of the 8 x 32 tile
-// (four 16-pixel k-steps) for its taps, with the next tap's A fragments and the next k-step's dY
-// fragments read while the current ones multiply — and 4 producer waves only stage: global
-// loads two tiles ahead in registers, bf16 hi/lo split, LDS stores into the other buffer. One
-// barrier per tile; the row pairs' partial sums meet in LDS in a fixed order (deterministic).
+// busy). Waves 0-3 only compute — wave c owns output rows 2c, 2c+1 of the 8 x 32 tile (four
+// 16-pixel k-steps, all 9 taps), with the next tap's A fragments and the next k-step's dY
+// fragments read while the current ones multiply — and waves 4-7 only stage: global loads two
+// tiles ahead in registers, bf16 hi/lo split, LDS stores into the other buffer. One barrier per
+// tile; the 4 consumers' partial sums meet in LDS in a fixed order (deterministic).
 __device__ __forceinline__ void pw_frag_pair(const unsigned char* plane, int plane_bytes, int row0,
                                              int lane, bf16x8& hi, bf16x8& lo) {
   hi = tr_frag_rows(plane, row0, lane);
   lo = tr_frag_rows(plane + plane_bytes, row0, lane);
 }
 
-// TG = 2: 8 consumer waves, two per SIMD — wave (row pair rp = wave % 4, tap group wave / 4)
-// owns taps 0-4 or 5-8 (5 accumulators): two independent MFMA streams per SIMD hide each other's
-// fragment-read latency (TG = 1: one consumer wave per SIMD, all 9 taps). 4 producer waves.
-template <int TG>
-__global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad_pc_kernel(
-    GemmConvParams p, int tiles, int tiles_per_split) {
-  constexpr int NC = 4 * TG;                 // consumer waves
-  constexpr int NA = TG == 1 ? 9 : 5;        // accumulators (taps) per consumer wave
+__global__ __launch_bounds__(512) void conv_x3_patch_wgrad_pc_kernel(GemmConvParams p, int tiles,
+                                                                     int tiles_per_split) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PW_STAGE];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -434,11 +428,9 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad_pc_kern
   const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
   const int n = t_end - t_begin;
 
-  const int rp = wave & 3, tg = wave >> 2;   // consumers: row pair, tap group
-  const int t0 = TG == 1 ? 0 : (tg ? 5 : 0), nt = TG == 1 ? 9 : (tg ? 4 : 5);
-  floatx16 acc[NA];  // consumers only (the producers' path never defines it: no registers)
-  if (wave >= NC) {  // ----------------------------------------------------------- producer
-    const int ptid = threadIdx.x - NC * 64;
+  floatx16 acc[9];  // consumers only (the producers' path never defines it: no registers)
+  if (wave >= 4) {  // ------------------------------------------------------------ producer
+    const int ptid = threadIdx.x - 256;
     const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + PT_H - 1) / PT_H;
     const long img_in = (long)p.h * p.w * cs;
     const long img_out = (long)p.oh * p.ow;
@@ -517,7 +509,7 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad_pc_kern
     }
   } else {  // ----------------------------------------------------------------- consumer
 #pragma unroll
-    for (int t = 0; t < NA; ++t)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     if (n > 0) {
@@ -525,39 +517,37 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad_pc_kern
       for (int t = 0; t < n; ++t) {
         const unsigned char* A = smem + (t & 1) * PW_STAGE;
         const unsigned char* B = A + 2 * PW_A;
-        // k-step s: output row 2 rp + (s >> 1), pixels 16 (s & 1) .. +15
+        // k-step s: output row 2 wave + (s >> 1), pixels 16 (s & 1) .. +15
         bf16x8 bh, bl, ah, al, nh, nl;
-        pw_frag_pair(B, PW_B, 32 * (2 * rp), lane, bh, bl);
-        pw_frag_pair(A, PW_A, (2 * rp + t0 / 3) * P_W + t0 % 3, lane, ah, al);
+        pw_frag_pair(B, PW_B, 32 * (2 * wave), lane, bh, bl);
+        pw_frag_pair(A, PW_A, (2 * wave) * P_W, lane, ah, al);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int row = 2 * rp + (s >> 1), px0 = 16 * (s & 1);
+          const int row = 2 * wave + (s >> 1), px0 = 16 * (s & 1);
           bf16x8 bh2 = bh, bl2 = bl;
           if (s < 3) {
             const int s1 = s + 1;
-            pw_frag_pair(B, PW_B, 32 * (2 * rp + (s1 >> 1)) + 16 * (s1 & 1), lane, bh2, bl2);
+            pw_frag_pair(B, PW_B, 32 * (2 * wave + (s1 >> 1)) + 16 * (s1 & 1), lane, bh2, bl2);
           }
 #pragma unroll
-          for (int i = 0; i < NA; ++i) {
-            if (i >= nt) break;  // wave-uniform (tap group 1 has 4 taps)
-            // the next A fragments (next tap, or the first tap of the next k-step) in flight
-            // during this tap's three products
-            if (i + 1 < nt) {
-              const int t1 = t0 + i + 1;
+          for (int tap = 0; tap < 9; ++tap) {
+            // the next A fragments (next tap, or tap 0 of the next k-step) in flight during
+            // this tap's three products
+            if (tap < 8) {
+              const int t1 = tap + 1;
               pw_frag_pair(A, PW_A, (row + t1 / 3) * P_W + px0 + t1 % 3, lane, nh, nl);
             } else if (s < 3) {
               const int s1 = s + 1;
-              pw_frag_pair(A, PW_A, (2 * rp + (s1 >> 1) + t0 / 3) * P_W + 16 * (s1 & 1) + t0 % 3,
-                           lane, nh, nl);
+              pw_frag_pair(A, PW_A, (2 * wave + (s1 >> 1)) * P_W + 16 * (s1 & 1), lane, nh, nl);
             }
             // the reads above issue before this tap's products (then the 3 MFMAs); one
             // fragment set ahead and no more: the scheduler otherwise hoists every read of the
             // tile (register blow-up, spills)
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS read
             __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
             ah = nh;
             al = nl;
             __builtin_amdgcn_sched_barrier(0);
@@ -569,24 +559,22 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad_pc_kern
       }
     }
   }
-  // the 4 row pairs' partial sums through LDS: each consumer writes its taps to its row pair's
-  // slot, then all threads add the 4 slots per element in a fixed order ((0 + 1) + (2 + 3)) and
-  // store (deterministic; no wave holds two sets of accumulators)
+  // the 4 consumers' partial sums through LDS: each writes its 9 tiles to its own slot, then
+  // all 512 threads add the 4 slots per element in a fixed order ((0 + 1) + (2 + 3)) and store
+  // (deterministic; no wave holds two sets of accumulators)
   constexpr int SLOT = 9 * 16 * 64;  // floats: tile t, register r, lane
   static_assert(4 * SLOT * 4 <= 2 * PW_STAGE, "reduction slots fit the staging LDS");
   float* red = reinterpret_cast<float*>(smem);
   __syncthreads();  // the last tile's LDS reads are done
-  if (wave < NC) {
+  if (wave < 4) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if (i >= nt) break;
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[rp * SLOT + ((t0 + i) * 16 + r) * 64 + lane] = acc[i][r];
-    }
+      for (int r = 0; r < 16; ++r) red[wave * SLOT + (t * 16 + r) * 64 + lane] = acc[t][r];
   }
   __syncthreads();
   float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
-  for (int e = threadIdx.x; e < SLOT; e += (NC + 4) * 64) {
+  for (int e = threadIdx.x; e < SLOT; e += 512) {
     const int ln = e & 63, r = (e >> 6) & 15, t = e >> 10;
     const int h = ln >> 5, col = n0 + (ln & 31);
     const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -630,13 +618,9 @@ constexpr int Q_A = Q_PIX * 64;        // patch plane: [204 px][32 ch] bf16
 constexpr int Q_B = Q_H * PT_W * 128;  // dY plane: [128 px][64 co] bf16
 constexpr int Q_STAGE = 2 * Q_A + 2 * Q_B;
 
-// TG = 2: 8 consumer waves (cout tile, row pair, tap group: taps 0-4 / 5-8), two per SIMD, as
-// conv_x3_patch_wgrad_pc_kernel<2>.
-template <int TG>
-__global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_kernel(
-    GemmConvParams p, int tiles, int tiles_per_split) {
-  constexpr int NC = 4 * TG;
-  constexpr int NA = TG == 1 ? 9 : 5;
+__global__ __launch_bounds__(512) void conv_x3_patch_wgrad64_pc_kernel(GemmConvParams p,
+                                                                       int tiles,
+                                                                       int tiles_per_split) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Q_STAGE];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -652,12 +636,11 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_ke
   const int n0 = nb * 64;
   const int t_begin = zb * tiles_per_split, t_end = min(tiles, t_begin + tiles_per_split);
   const int n = t_end - t_begin;
-  const int ct = wave & 1, rp = (wave >> 1) & 1, tg = wave >> 2;
-  const int t0 = TG == 1 ? 0 : (tg ? 5 : 0), nt = TG == 1 ? 9 : (tg ? 4 : 5);
+  const int ct = wave & 1, rp = (wave >> 1) & 1;
 
-  floatx16 acc[NA];
-  if (wave >= NC) {  // ----------------------------------------------------------- producer
-    const int ptid = threadIdx.x - NC * 64;
+  floatx16 acc[9];
+  if (wave >= 4) {  // ------------------------------------------------------------ producer
+    const int ptid = threadIdx.x - 256;
     const int tiles_x = (p.ow + PT_W - 1) / PT_W, tiles_y = (p.oh + Q_H - 1) / Q_H;
     const long img_in = (long)p.h * p.w * cs;
     const long img_out = (long)p.oh * p.ow;
@@ -734,7 +717,7 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_ke
     }
   } else {  // ----------------------------------------------------------------- consumer
 #pragma unroll
-    for (int t = 0; t < NA; ++t)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     if (n > 0) {
@@ -746,7 +729,7 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_ke
         bf16x8 bh, bl, ah, al, nh, nl;
         bh = tr_frag_dy64(B, 32 * (2 * rp), 32 * ct, lane);
         bl = tr_frag_dy64(B + Q_B, 32 * (2 * rp), 32 * ct, lane);
-        pw_frag_pair(A, Q_A, (2 * rp + t0 / 3) * P_W + t0 % 3, lane, ah, al);
+        pw_frag_pair(A, Q_A, (2 * rp) * P_W, lane, ah, al);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int row = 2 * rp + (s >> 1), px0 = 16 * (s & 1);
@@ -757,21 +740,19 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_ke
             bl2 = tr_frag_dy64(B + Q_B, k1, 32 * ct, lane);
           }
 #pragma unroll
-          for (int i = 0; i < NA; ++i) {
-            if (i >= nt) break;  // wave-uniform
-            if (i + 1 < nt) {
-              const int t1 = t0 + i + 1;
+          for (int tap = 0; tap < 9; ++tap) {
+            if (tap < 8) {
+              const int t1 = tap + 1;
               pw_frag_pair(A, Q_A, (row + t1 / 3) * P_W + px0 + t1 % 3, lane, nh, nl);
             } else if (s < 3) {
               const int s1 = s + 1;
-              pw_frag_pair(A, Q_A, (2 * rp + (s1 >> 1) + t0 / 3) * P_W + 16 * (s1 & 1) + t0 % 3,
-                           lane, nh, nl);
+              pw_frag_pair(A, Q_A, (2 * rp + (s1 >> 1)) * P_W + 16 * (s1 & 1), lane, nh, nl);
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS read
             __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[tap], 0, 0, 0);
+            acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[tap], 0, 0, 0);
             ah = nh;
             al = nl;
             __builtin_amdgcn_sched_barrier(0);
@@ -784,34 +765,30 @@ __global__ __launch_bounds__((4 * TG + 4) * 64) void conv_x3_patch_wgrad64_pc_ke
     }
   }
   // row pair 1 -> LDS slot of its cout tile; row pair 0 adds it in place ((rp 0) + (rp 1)); then
-  // all threads store both cout tiles (deterministic; the tap groups' taps are disjoint)
+  // all 512 threads store both cout tiles (deterministic)
   constexpr int SLOT = 9 * 16 * 64;  // floats: tile t, register r, lane
   static_assert(2 * SLOT * 4 <= 2 * Q_STAGE, "reduction slots fit the staging LDS");
   float* red = reinterpret_cast<float*>(smem);
   __syncthreads();  // the last tile's LDS reads are done
-  if (wave < NC && rp == 1) {
+  if (wave < 4 && rp == 1) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if (i >= nt) break;
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[ct * SLOT + ((t0 + i) * 16 + r) * 64 + lane] = acc[i][r];
-    }
+      for (int r = 0; r < 16; ++r) red[ct * SLOT + (t * 16 + r) * 64 + lane] = acc[t][r];
   }
   __syncthreads();
-  if (wave < NC && rp == 0) {
+  if (wave < 4 && rp == 0) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if (i >= nt) break;
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float* e = red + ct * SLOT + ((t0 + i) * 16 + r) * 64 + lane;
-        *e = acc[i][r] + *e;
+        float* e = red + ct * SLOT + (t * 16 + r) * 64 + lane;
+        *e = acc[t][r] + *e;
       }
-    }
   }
   __syncthreads();
   float* out = p.out1 + (p.zstride > 0 ? (long)zb * p.zstride : 0);
-  for (int e = threadIdx.x; e < 2 * SLOT; e += (NC + 4) * 64) {
+  for (int e = threadIdx.x; e < 2 * SLOT; e += 512) {
     const int c2t = e / SLOT, f = e - c2t * SLOT;
     const int ln = f & 63, r = (f >> 6) & 15, t = f >> 10;
     const int h = ln >> 5, col = n0 + 32 * c2t + (ln & 31);
@@ -930,20 +907,15 @@ extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* s
   }
   const int tiles = pld__x3_patch_wgrad_tiles(p);
   const int tps = (int)cdiv(tiles, splits);
-#ifndef X3_PW_TG
-#define X3_PW_TG 2  // consumer waves per SIMD of the patch WGRAD kernels
-#endif
   p->kc1 = (int)cdiv(p->c1, 32);
   const int chunks = p->kc1 + (int)cdiv(p->c2, 32);
   if (pld__x3_patch_wgrad_cw(p->N) == 64) {
     dim3 grid(chunks, cdiv(p->N, 64), cdiv(tiles, tps));
-    x3::conv_x3_patch_wgrad64_pc_kernel<X3_PW_TG>
-        <<<grid, (4 * X3_PW_TG + 4) * 64, 0, as_stream(stream)>>>(*p, tiles, tps);
+    x3::conv_x3_patch_wgrad64_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
     return check_launch("conv_x3_patch_wgrad64_pc_kernel");
   }
   dim3 grid(chunks, cdiv(p->N, 32), cdiv(tiles, tps));
-  x3::conv_x3_patch_wgrad_pc_kernel<X3_PW_TG>
-      <<<grid, (4 * X3_PW_TG + 4) * 64, 0, as_stream(stream)>>>(*p, tiles, tps);
+  x3::conv_x3_patch_wgrad_pc_kernel<<<grid, 512, 0, as_stream(stream)>>>(*p, tiles, tps);
   return check_launch("conv_x3_patch_wgrad_pc_kernel");
 }
 // sk_grid > 0: the tile-stream schedule with that many workgroups (p->sk_* filled by the host;

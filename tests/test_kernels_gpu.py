@@ -483,11 +483,10 @@ def test_bn_forward_backward(cuda, rows, c, act):
 
 
 @pytest.mark.parametrize("rows,c", [(401408, 24), (6272, 1152), (777, 40)])
-def test_bn_in_kernel_finalize_repeats(cuda, rows, c):
-    """The reductions finalize inside chan_reduce_kernel (two levels of last-arriving
-    workgroups on self-resetting tickets): repeated eager launches and replays of a captured
-    graph give bit-identical statistics, coefficients and gradients (the tickets are back at
-    zero after every launch; the summation order does not depend on who arrives last)."""
+def test_bn_reductions_repeat_bitwise(cuda, rows, c):
+    """BN statistics, BN backward and the channel sum (fp64 partials, fixed-order finalize):
+    repeated eager launches and replays of a captured graph give bit-identical statistics,
+    coefficients and gradients, one and two channel columns, tens to thousands of partials."""
     g = torch.Generator(device=cuda).manual_seed(rows + c)
     x = torch.randn(rows, c, device=cuda, generator=g) * 2 + 0.5
     dy = torch.randn(rows, c, device=cuda, generator=g)

@@ -7,6 +7,7 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tk.log 2>&1 || { tail -30 $O/tk.log; exit 1; }
 tail -2 $O/tk.log
 bash tools/gpu_r4j.sh || exit 1
+bash tools/gpu_r4k.sh || exit 1
 for v in pwtg1 new; do
   L=""; [ $v != new ] && L=ab/$v/libpldepth_hip.so
   for args in "--h 56 --w 56 --c1 240 --c2 240 --cout 144" "--h 112 --w 112 --c1 144 --c2 144 --cout 32" "--h 224 --w 224 --c1 32 --cout 32" "--h 28 --w 28 --c1 672 --c2 672 --cout 240"; do
