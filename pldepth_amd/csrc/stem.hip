@@ -7,11 +7,11 @@
 // 3 input channels make the im2col GEMM K = 27: an MFMA tile pads it to 32 and re-reads the map
 // per tap (conv_igemm_kernel: 0.22 ms at 448^2 x 32, 1.3 TB/s). Here a 256-thread workgroup owns
 // an 8 x 32 output tile: it stages the 17 x 65 x 3 input window once (coalesced rows, prologue
-// applied, padding zeros), each thread holds one output pixel's 27 taps in registers and forms its
-// 32 channels with the filter as scalar (SGPR) operands, one channel's 27 contiguous weights at a
-// time (a tap-outer order would need 32 strided scalar loads per tap: 164 us, latency-bound) —
-// exact fp32 fmaf chains in (ty, tx, ci) order, like the exact-fp32 GEMM path — and the [256][32]
-// tile leaves through LDS as contiguous 4 KB row runs.
+// applied, padding zeros; all loads of a thread in flight together: a rolled loop waiting out
+// each load's latency ran 164 us), each thread holds one output pixel's 27 taps in registers and
+// forms its 32 channels with the filter as scalar (SGPR) operands, one channel's 27 contiguous
+// weights at a time, accumulating in fp64 with one rounding per output, and the [256][32] tile
+// leaves through LDS as contiguous 4 KB row runs.
 // Algorithmic bytes: the input once + the output once (77 + 205 MB at 448^2 x 32).
 #include <algorithm>
 
@@ -97,13 +97,18 @@ __global__ __launch_bounds__(256) void stem3x3_kernel(Params p) {
 #pragma unroll
       for (int ci = 0; ci < CI; ++ci)
         xv[(ty * KS + tx) * CI + ci] = xin[((ly * S + ty) * IW + lx * S + tx) * CI + ci];
+  // fp64 accumulation, one rounding to fp32 per output: the stem's output is then within half
+  // an ulp of the exact sum, whatever order an fp32 chain would take (the 64^2 batch-2 parity
+  // test amplifies the stem's rounding through a training-mode BN over 8 values per channel at
+  // top_activation). The 864 fp64 FMAs per pixel stay hidden under the kernel's HBM time.
   float acc[CO];
 #pragma unroll
   for (int co = 0; co < CO; ++co) {
-    float a = 0.f;
+    double a = 0.0;
 #pragma unroll
-    for (int t = 0; t < KS * KS * CI; ++t) a = fmaf(xv[t], p.w[co * KS * KS * CI + t], a);
-    acc[co] = a;
+    for (int t = 0; t < KS * KS * CI; ++t)
+      a = fma((double)xv[t], (double)p.w[co * KS * KS * CI + t], a);
+    acc[co] = (float)a;
   }
   __syncthreads();  // the window is dead: the output tile takes its space
 #pragma unroll

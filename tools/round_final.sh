@@ -1,16 +1,19 @@
 # Round-end evidence (GPU box): full GPU test suite, default bench line (with cpu_baseline),
 # rocprofv3 kernel trace + per-step kstats, PMC traffic of one eager step + the dominant kernel's
-# HBM vs algorithmic bytes, ff_redweb kernel trace. bash tools/round_final.sh TAG
+# HBM vs algorithmic bytes, ff_redweb kernel trace. bash tools/round_final.sh TAG [--no-tests]
 TAG=${1:-final}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-export PLD_REPORT_DIR=$O/parity
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
-rc=$?
-tail -3 $O/gputest.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+rc=0
+if [ "$2" != "--no-tests" ]; then
+  export PLD_REPORT_DIR=$O/parity
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
+  rc=$?
+  tail -3 $O/gputest.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || exit 1
 tail -c 600 $O/bench.json
@@ -31,3 +34,4 @@ rm -rf $O/trace
 bash $R/tools/prof_redweb.sh ${TAG}_rw > /dev/null 2>&1 || exit 1
 head -3 $R/gpurun_out/prof_${TAG}_rw/kstats.txt
 echo done
+exit $rc
