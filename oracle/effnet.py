@@ -132,23 +132,27 @@ def _bn(P, name, x):
                     P[name + "/moving_variance"])
 
 
-def forward(P, x_nhwc, drop_scales=None, taps=None, training=True, bn_stats=None):
+def forward(P, x_nhwc, drop_scales=None, taps=None, training=True, bn_stats=None,
+            relu_masks=None):
     """ff_effnet forward. P: dict of fp64 tensors (Keras names/layouts). x_nhwc: [N,H,W,3] in
     [0,1]. drop_scales: {block_name: [N] keep/(1-rate) factors} (None = drop-connect off).
     taps: optional dict receiving intermediate NHWC activations. training=False: every BN on
     its moving statistics (Keras predict / validation; drop-connect is then off). bn_stats:
-    optional dict receiving every training-mode BN's batch mean and variance. Returns
+    optional dict receiving every training-mode BN's batch mean and variance. relu_masks:
+    optional {decoder stage: [N,C,H,W] 0/1} replacing that stage's ReLU by a multiplication
+    with the given mask (the same piecewise-linear branch as another implementation took, for
+    comparing arithmetic where a pre-activation lies within rounding of 0). Returns
     [N,H,W,1]."""
     if bn_stats is not None:
         _STATS[0] = bn_stats
         try:
-            return forward(P, x_nhwc, drop_scales, taps, training)
+            return forward(P, x_nhwc, drop_scales, taps, training, relu_masks=relu_masks)
         finally:
             _STATS[0] = None
     if not training:
         _TRAINING[0] = False
         try:
-            return forward(P, x_nhwc, None, taps, True)
+            return forward(P, x_nhwc, None, taps, True, relu_masks=relu_masks)
         finally:
             _TRAINING[0] = True
     acts = taps if taps is not None else {}
@@ -191,7 +195,12 @@ def forward(P, x_nhwc, drop_scales=None, taps=None, training=True, bn_stats=None
     acts["top_activation"] = x
     for i, (name, cout, skip) in enumerate(DECODER):
         x = conv_same(x, P[name + "/kernel"], P[name + "/bias"])
-        x = torch.relu(_bn(P, f"dec_bn{i}", x))
+        z = _bn(P, f"dec_bn{i}", x)
+        acts[f"dec{i}_z"] = z  # the pre-activation (its sign decides the ReLU branch)
+        if relu_masks is not None and i in relu_masks:
+            x = z * relu_masks[i].to(z.dtype)
+        else:
+            x = torch.relu(z)
         x = up2(x)
         if skip is not None:
             x = torch.cat([x, acts[skip]], dim=1)
@@ -206,10 +215,11 @@ def trainable_names(P):
     return [k for k in P if k.startswith("dec_conv") or k.endswith("/gamma") or k.endswith("/beta")]
 
 
-def train_step_grads(P, x_nhwc, dloss_dpred, drop_scales=None):
-    """Gradients of the trainable parameters for an upstream gradient dloss/dpred (fp64)."""
+def train_step_grads(P, x_nhwc, dloss_dpred, drop_scales=None, relu_masks=None):
+    """Gradients of the trainable parameters for an upstream gradient dloss/dpred (fp64);
+    relu_masks as in forward."""
     Q = {k: (v.detach().clone().requires_grad_(True) if k in set(trainable_names(P))
              else v.detach()) for k, v in P.items()}
-    out = forward(Q, x_nhwc, drop_scales)
+    out = forward(Q, x_nhwc, drop_scales, relu_masks=relu_masks)
     out.backward(dloss_dpred)
     return {k: Q[k].grad.detach() for k in trainable_names(P)}, out.detach()

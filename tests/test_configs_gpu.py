@@ -91,21 +91,24 @@ def _nonuniform(drop):
 ILL_CONDITIONED = {"dec_conv4/kernel"}
 
 
-def check_gradients(tag, hip, g64, g32, structural_zero):
-    """The bar of the module docstring; returns the per-tensor report."""
+def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None):
+    """The bar of the module docstring; returns the per-tensor report. g64_32: the fp64
+    reference the fp32 restatement is measured against (default g64; the flip-aware form gives
+    each implementation the fp64 gradient along its own decoder ReLU branches)."""
+    g64_32 = g64 if g64_32 is None else g64_32
     keys = [k for k in g64 if not structural_zero(k)]
     rows, fails = {}, []
     for k in keys:
-        e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64[k])
+        e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64_32[k])
         bar = TOL if e32 <= TOL and k not in ILL_CONDITIONED else max(TOL, 4.0 * e32)
         rows[k] = {"hip": e_hip, "fp32_restatement": e32, "bar": bar}
         if e_hip > bar:
             fails.append((k, e_hip, e32))
     flat = lambda g: torch.cat([torch.as_tensor(g[k]).detach().double().cpu().flatten()
                                 for k in keys])
-    a, b, c = flat(hip), flat(g64), flat(g32)
+    a, b, c, b32 = flat(hip), flat(g64), flat(g32), flat(g64_32)
     glob = {"hip_rel_l2": float((a - b).norm() / b.norm()),
-            "fp32_rel_l2": float((c - b).norm() / b.norm()),
+            "fp32_rel_l2": float((c - b32).norm() / b32.norm()),
             "cos": float(a @ b / (a.norm() * b.norm())),
             "tensors": len(keys),
             "tensors_fp32_within_1e-3": sum(r["fp32_restatement"] <= TOL for r in rows.values()),
@@ -114,7 +117,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero):
     for k in g64:
         if structural_zero(k):
             assert float(torch.as_tensor(hip[k]).abs().max()) <= 1e-3 * scale + 1e-6, k
-    report(tag, {"global": glob, "tensors": rows})
+    report(tag, dict({"global": glob, "tensors": rows}, **(extra or {})))
     print(f"[{tag}] {glob}")
     assert not fails, fails[:10]
     assert glob["hip_rel_l2"] <= max(TOL, 2.0 * glob["fp32_rel_l2"])
@@ -122,7 +125,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero):
 
 
 # ------------------------------------------------------------ cfg2 arithmetic at 448x448
-def test_effnet_448_bf16x3_gradients(cuda):
+def test_effnet_448_bf16x3_gradients(cuda, fixed_schedules):
     B, H, R, L = 2, 448, 100, 5
     eng = EffNetFF((H, H, 3), B, seed=0, conv_math="bf16x3")
     eng.drop_connect = False
@@ -151,6 +154,20 @@ def test_effnet_448_bf16x3_gradients(cuda):
 
 
 # ------------------------------------------------------------------- drop-connect
+def hip_decoder_relu_masks(eng, weights):
+    """The decoder ReLU branches the HIP forward took: z = BN(dec{i}_pre) > 0 with the step's
+    batch statistics and the pre-update gamma / beta, as [N, C, H, W] masks for
+    OE.forward(relu_masks=...)."""
+    out = {}
+    for i, (conv, bn, skip) in enumerate(eng.dec):
+        pre = eng.act[f"dec{i}_pre"].double().cpu()
+        ga = torch.tensor(weights[f"dec_bn{i}/gamma"], dtype=torch.float64)
+        be = torch.tensor(weights[f"dec_bn{i}/beta"], dtype=torch.float64)
+        z = (pre - bn.mean.double().cpu()) * bn.invstd.double().cpu() * ga + be
+        out[i] = (z > 0).permute(0, 3, 1, 2).double()
+    return out
+
+
 def _residual_drop_blocks(eng):
     return [(li, blk) for li, blk in enumerate(eng.blocks) if blk["residual"] and blk["rate"] > 0]
 
@@ -185,7 +202,7 @@ def test_sampler_draws_bit_exact_vs_philox(cuda):
                                   PX.sampler_draws(nv, 500, 5, 1234, (1 << 33) + 7, 5))
 
 
-def test_dropconnect_forward_and_gradients(cuda):
+def test_dropconnect_forward_and_gradients(cuda, fixed_schedules):
     """Drop-connect as the timed step runs it: the per-block (step, image)-keyed scales read
     back from the engine and injected into the oracle."""
     B, H, R, L, seed = 4, 128, 24, 5, 0
@@ -233,7 +250,7 @@ def test_dropconnect_forward_and_gradients(cuda):
 
 
 # ------------------------------------------------------------------- cfg1: whole step
-def test_cfg1_trainer_step_224(cuda):
+def test_cfg1_trainer_step_224(cuda, fixed_schedules):
     """BASELINE cfg1 (ff_effnet 224x224, B=2, L=2, R=100, Info sampler): one eager
     ReplicaTrainer step — GPU sampler, forward with drop-connect, ListMLE, backward, Adam —
     against the oracle chain fed the same Philox draws and drop scales."""
@@ -272,13 +289,40 @@ def test_cfg1_trainer_step_224(cuda):
         pred_ref = OE.forward(P, x64, drop_scales=drop)
     loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
     assert abs(tr.loss_value() - loss_ref) / abs(loss_ref) < TOL
-    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
+    # Flip-aware reference: at 224^2 batch 2 a few decoder pre-activations lie within rounding
+    # of 0 (dec3: 21 of 200704 within 1e-5 of the largest), and a pixel whose ReLU branch differs
+    # passes its whole gradient in one realization and none in the other. One such pixel in a
+    # channel whose beta gradient cancels to a small sum sets that tensor's max error
+    # (tools/exp_relu_flips.py: the worst dec_bn{i}/beta channel holds a flipped pixel at every
+    # stage; the fp32 restatement flips 3-33 pixels per stage, HIP 1-13). Each implementation is
+    # therefore measured against the fp64 gradient along ITS OWN decoder ReLU branches; the
+    # plain comparison stays in the report.
+    drop32 = {k: v.float() for k, v in drop.items()}
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    taps32 = {}
+    with torch.no_grad():
+        OE.forward(P32, torch.tensor(x), drop_scales=drop32, taps=taps32)
+    m32 = {i: (taps32[f"dec{i}_z"] > 0).double() for i in range(len(eng.dec))}
+    mh = hip_decoder_relu_masks(eng, weights)
+    g64h, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop,
+                                  relu_masks=mh)
+    g64f, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop,
+                                  relu_masks=m32)
+    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
     g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
-                                 drop_scales={k: v.float() for k, v in drop.items()})
+                                 drop_scales=drop32)
     nu = _nonuniform(drop)
-    check_gradients("cfg1_224", {k: eng.grads[k] for k in g64}, g64, g32,
-                    lambda k: effnet_structural_zero(k, nu))
+    with torch.no_grad():
+        taps64 = {}
+        OE.forward(P, x64, drop_scales=drop, taps=taps64)
+    flips = {f"dec{i}": {"hip": int(((mh[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum()),
+                         "fp32": int(((m32[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum())}
+             for i in range(len(eng.dec))}
+    plain = {k: {"hip": rel(eng.grads[k], g64[k]), "fp32_restatement": rel(g32[k], g64[k])}
+             for k in g64}
+    check_gradients("cfg1_224", {k: eng.grads[k] for k in g64}, g64h, g32,
+                    lambda k: effnet_structural_zero(k, nu), g64_32=g64f,
+                    extra={"relu_flips_vs_fp64": flips, "plain_comparison": plain})
     # Adam-AMSGrad (step 1) applied by the oracle to the step's own gradients
     z = np.zeros(params0.numel(), np.float32)
     p_ref, *_ = adam_amsgrad_step(params0.cpu().numpy(), eng.grads.buf.cpu().numpy(), z, z, z,
@@ -288,7 +332,7 @@ def test_cfg1_trainer_step_224(cuda):
 
 
 # ------------------------------------------------------------------- cfg3: ff_redweb 448
-def test_cfg3_redweb_448(cuda):
+def test_cfg3_redweb_448(cuda, fixed_schedules):
     """Whole training step at batch 2 with the encoder in exact fp32 and the decoder bf16x3
     ('mixed'). With bf16x3 in the early encoder too, conv5_block3_out lands 1.2e-3 from fp64 at
     this batch: the conv4/conv5 BNs normalise over 28*28*2 / 14*14*2 values per channel and
