@@ -125,10 +125,37 @@ def maxpool_zero_padded(x, k=3, s=2, pad=1):
     return F.max_pool2d(F.pad(x, (pad, pad, pad, pad)), k, s)
 
 
-def encoder(P, x, acts):
+def _relu(x, site, masks=None, branches=None):
+    """ReLU at a named site (the HIP engine's buffer name for its output). masks: optional
+    {site: [N,C,H,W] bool} replacing the ReLU by a multiplication with the given branch mask (the
+    branches another implementation took, for comparing arithmetic where a pre-activation lies
+    within rounding of 0); branches: optional dict receiving {site: x > 0} (this run's own)."""
+    if branches is not None:
+        branches[site] = (x > 0).detach()
+    if masks is not None and site in masks:
+        return x * masks[site].to(x.dtype)
+    return torch.relu(x)
+
+
+def relu_sites():
+    """Every ReLU site of the forward, by the HIP engine's output-buffer name."""
+    out = ["conv1_relu"]
+    for name, f, blocks, stride1 in RESNET50_STACKS:
+        for b in range(1, blocks + 1):
+            pre = f"{name}_block{b}_"
+            out += [pre + "1_relu", pre + "2_relu", pre + "out"]
+    for name, *_ in FFLS:
+        for part in ("block_left", "block_down"):
+            for half in (0, 3):
+                n = f"{name}/{part}"
+                out += [f"{n}/act{half}", f"{n}/act{half + 1}", f"{n}/out{half}"]
+    return out + ["aol/act0"]
+
+
+def encoder(P, x, acts, masks=None, branches=None):
     """x: NCHW preprocessed input. Fills acts with every block output; returns the taps."""
     x = conv(x, P["conv1_conv/kernel"], P["conv1_conv/bias"], 2, (3, 3, 3, 3))
-    x = torch.relu(_bn(P, "conv1_bn", x, RESNET_BN_EPS))
+    x = _relu(_bn(P, "conv1_bn", x, RESNET_BN_EPS), "conv1_relu", masks, branches)
     acts["conv1_relu"] = x
     x = maxpool_zero_padded(x)
     acts["pool1_pool"] = x
@@ -142,52 +169,54 @@ def encoder(P, x, acts):
             else:
                 sc = x
             y = conv(x, P[pre + "1_conv/kernel"], P[pre + "1_conv/bias"], s)
-            y = torch.relu(_bn(P, pre + "1_bn", y, RESNET_BN_EPS))
+            y = _relu(_bn(P, pre + "1_bn", y, RESNET_BN_EPS), pre + "1_relu", masks, branches)
             y = conv_same(y, P[pre + "2_conv/kernel"], P[pre + "2_conv/bias"])
-            y = torch.relu(_bn(P, pre + "2_bn", y, RESNET_BN_EPS))
+            y = _relu(_bn(P, pre + "2_bn", y, RESNET_BN_EPS), pre + "2_relu", masks, branches)
             y = conv(y, P[pre + "3_conv/kernel"], P[pre + "3_conv/bias"])
             y = _bn(P, pre + "3_bn", y, RESNET_BN_EPS)
-            x = torch.relu(sc + y)
+            x = _relu(sc + y, pre + "out", masks, branches)
             acts[pre + "out"] = x
     return [acts[t] for t in TAPS]
 
 
-def bottleneck(P, name, x):
+def bottleneck(P, name, x, masks=None, branches=None):
     """BottleneckConvLayer.call (redweb.py:137-165)."""
     for half in (0, 3):
         res = x
-        out = torch.relu(_bn(P, f"{name}/bn{half}", conv(x, P[f"{name}/conv{half}/kernel"]),
-                             DEC_BN_EPS))
-        out = torch.relu(_bn(P, f"{name}/bn{half + 1}",
-                             conv_same(out, P[f"{name}/conv{half + 1}/kernel"]), DEC_BN_EPS))
+        out = _relu(_bn(P, f"{name}/bn{half}", conv(x, P[f"{name}/conv{half}/kernel"]),
+                        DEC_BN_EPS), f"{name}/act{half}", masks, branches)
+        out = _relu(_bn(P, f"{name}/bn{half + 1}",
+                        conv_same(out, P[f"{name}/conv{half + 1}/kernel"]), DEC_BN_EPS),
+                    f"{name}/act{half + 1}", masks, branches)
         out = _bn(P, f"{name}/bn{half + 2}", conv(out, P[f"{name}/conv{half + 2}/kernel"]),
                   DEC_BN_EPS)
-        x = torch.relu(out + res)
+        x = _relu(out + res, f"{name}/out{half}", masks, branches)
     return x
 
 
-def ffl(P, name, in_left, in_up):
+def ffl(P, name, in_left, in_up, masks=None, branches=None):
     """FeatureFusionLayer.call (redweb.py:261-273)."""
     left = _bn(P, name + "/bn0", conv_same(in_left, P[name + "/conv0/kernel"]), DEC_BN_EPS)
-    left = bottleneck(P, name + "/block_left", left)
+    left = bottleneck(P, name + "/block_left", left, masks, branches)
     up = _bn(P, name + "/bn1", conv_same(in_up, P[name + "/conv1/kernel"]), DEC_BN_EPS)
-    return up2(bottleneck(P, name + "/block_down", left + up))
+    return up2(bottleneck(P, name + "/block_down", left + up, masks, branches))
 
 
-def forward(P, x_nhwc, taps=None, preprocessed=False):
+def forward(P, x_nhwc, taps=None, preprocessed=False, relu_masks=None, relu_branches=None):
     """ff_redweb forward. P: fp64 tensors by name (param_specs). x_nhwc [N,H,W,3] in [0,1]
-    (caffe preprocessing applied here unless preprocessed=True). Returns [N,H,W,1]."""
+    (caffe preprocessing applied here unless preprocessed=True). relu_masks / relu_branches:
+    as _relu, by relu_sites() name. Returns [N,H,W,1]."""
     acts = taps if taps is not None else {}
     if not preprocessed:
         x_nhwc = caffe_preprocess(x_nhwc)
     x = x_nhwc.permute(0, 3, 1, 2)
-    g2, g3, g4, g5 = encoder(P, x, acts)
+    g2, g3, g4, g5 = encoder(P, x, acts, relu_masks, relu_branches)
     b = up2(g5)
     for (name, _, _, _, _, _), left in zip(FFLS, (g4, g3, g2)):
-        b = ffl(P, name, left, b)
+        b = ffl(P, name, left, b, relu_masks, relu_branches)
         acts[name] = b
     x = conv_same(b, P["aol/conv0/kernel"], P["aol/conv0/bias"])
-    x = torch.relu(_bn(P, "aol/bn0", x, DEC_BN_EPS))
+    x = _relu(_bn(P, "aol/bn0", x, DEC_BN_EPS), "aol/act0", relu_masks, relu_branches)
     x = conv_same(x, P["aol/conv1/kernel"], P["aol/conv1/bias"])
     x = up2(x)
     x = conv(x, P["aol/conv2/kernel"], P["aol/conv2/bias"])
@@ -198,11 +227,11 @@ def trainable_names(P=None):
     return [n for n, _, kind in param_specs() if kind == "trainable"]
 
 
-def train_step_grads(P, x_nhwc, dloss_dpred, preprocessed=False):
+def train_step_grads(P, x_nhwc, dloss_dpred, preprocessed=False, relu_masks=None):
     names = set(trainable_names())
     Q = {k: (v.detach().clone().requires_grad_(True) if k in names else v.detach())
          for k, v in P.items()}
-    out = forward(Q, x_nhwc, preprocessed=preprocessed)
+    out = forward(Q, x_nhwc, preprocessed=preprocessed, relu_masks=relu_masks)
     out.backward(dloss_dpred)
     return {k: Q[k].grad.detach() for k in names}, out.detach()
 

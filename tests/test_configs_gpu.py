@@ -14,8 +14,7 @@
 
 Gradient bar (BASELINE.json: 1e-3 relative): per tensor 1e-3 wherever the fp32 restatement of
 the reference semantics itself lands within 1e-3 of fp64, else 4x the fp32 restatement's own
-error (also for the measured ill-conditioned tensors of ILL_CONDITIONED); over all tensors
-together a global rel-L2 within max(1e-3, 2x the fp32 restatement's).
+error; over all tensors together a global rel-L2 within max(1e-3, 2x the fp32 restatement's).
 The gradients of the reference semantics are themselves ill-conditioned at the 1e-3 level:
 training-mode BN cancels most of each incoming gradient, and
 an exact fp32 implementation lands ~1 % (median per tensor) from fp64 at batch 2 AND at the
@@ -23,6 +22,13 @@ bench's batch 32 (ff_effnet 5 of 98 tensors within 1e-3, ff_redweb 3 of 237; pro
 bf16x3 products carry ~2^8 the rounding of fp32 ones; measured HIP / fp32-restatement error
 ratios: median 0.90 (ff_effnet) / 1.03 (ff_redweb) at batch 32, worst 2.3. Reports of every tensor
 are written to $PLD_REPORT_DIR when set.
+Round 4 found where that ill-conditioning comes from for ff_effnet: decoder pre-activations within
+rounding of 0 take the other ReLU branch in one implementation (one such pixel passes its whole
+gradient or none of it). Measured against the fp64 gradient along each implementation's OWN
+decoder ReLU branches (the oracle's relu_masks), every cfg1 tensor of both HIP and the fp32
+restatement lands within 1e-3 (HIP global rel-L2 8.6e-5); the ff_effnet tests here use that
+flip-aware reference with the strict 1e-3 bar and report the plain comparison and the flip counts
+beside it. ff_redweb has ReLUs throughout the encoder too and keeps the plain comparison.
 """
 import json
 import os
@@ -79,16 +85,10 @@ def _nonuniform(drop):
     return {k for k, v in drop.items() if float(v.max()) != float(v.min())}
 
 
-# Tensors whose distance from fp64 is set by fp32-level rounding anywhere upstream, documented
-# by measurement (profiles/r04_dec_precision.txt, tools/exp_dec_precision.py): ff_effnet's
-# dec_conv4/kernel at batch 32 sits at 9.3e-4 in the torch-CPU fp32 restatement and 7.0e-4 with
-# every HIP conv in exact fp32, and moves between 6.7e-4 and 1.84e-3 when the arithmetic of ONE
-# upstream layer changes (dec_conv0 or dec_conv2 forward in fp32: 6.7e-4; all decoder convs in
-# fp32: 1.84e-3; the bench's bf16x3: 1.84e-3); the dW kernel's own arithmetic is 9.5e-7 from
-# fp64 on the same operands, and the error sits in one output channel (cout 31). Such a tensor
-# gets 4x the fp32 restatement's error instead of 1e-3; every other tensor whose fp32
-# restatement meets 1e-3 is held to 1e-3.
-ILL_CONDITIONED = {"dec_conv4/kernel"}
+# (round 3 kept dec_conv4/kernel as an "ill-conditioned" exception: its plain distance from fp64
+# moved between 6.7e-4 and 1.84e-3 with the arithmetic of one upstream layer. Round 4 traced it
+# to decoder ReLU branch flips: along HIP's own branches it is 1.4e-5 from fp64 at batch 32, and
+# the ff_effnet tests compare flip-aware with no exception.)
 
 
 def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None):
@@ -100,7 +100,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
     rows, fails = {}, []
     for k in keys:
         e_hip, e32 = rel(hip[k], g64[k]), rel(g32[k], g64_32[k])
-        bar = TOL if e32 <= TOL and k not in ILL_CONDITIONED else max(TOL, 4.0 * e32)
+        bar = TOL if e32 <= TOL else 4.0 * e32
         rows[k] = {"hip": e_hip, "fp32_restatement": e32, "bar": bar}
         if e_hip > bar:
             fails.append((k, e_hip, e32))
@@ -145,11 +145,8 @@ def test_effnet_448_bf16x3_gradients(cuda, fixed_schedules):
     loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
     assert rel(pred, pred_ref) < TOL
     assert abs(loss.item() - loss_ref) / abs(loss_ref) < TOL
-    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref))
-    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
-    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float())
-    hip = {k: eng.grads[k] for k in g64}
-    glob = check_gradients("effnet448_bf16x3", hip, g64, g32, effnet_structural_zero)
+    glob = effnet_grads_flip_aware("effnet448_bf16x3", eng, weights, x, dpred_ref,
+                                   effnet_structural_zero)
     assert glob["cos"] > 0.9999
 
 
@@ -166,6 +163,37 @@ def hip_decoder_relu_masks(eng, weights):
         z = (pre - bn.mean.double().cpu()) * bn.invstd.double().cpu() * ga + be
         out[i] = (z > 0).permute(0, 3, 1, 2).double()
     return out
+
+
+def effnet_grads_flip_aware(tag, eng, weights, x, dpred_ref, structural_zero, drop=None):
+    """check_gradients for an ff_effnet step against the flip-aware reference: HIP vs the fp64
+    gradient along HIP's decoder ReLU branches, the fp32 restatement vs fp64 along its own, the
+    strict 1e-3 bar; the plain comparison and the per-stage ReLU flip counts go to the report."""
+    mh = hip_decoder_relu_masks(eng, weights)
+    hip = {k: eng.grads[k] for k in OE.trainable_names(weights)}
+    P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
+    x64, x32 = torch.tensor(x, dtype=torch.float64), torch.tensor(x)
+    d64 = torch.tensor(dpred_ref, dtype=torch.float64)
+    drop32 = None if drop is None else {k: v.float() for k, v in drop.items()}
+    taps64, taps32 = {}, {}
+    with torch.no_grad():
+        OE.forward(P, x64, drop_scales=drop, taps=taps64)
+        OE.forward(P32, x32, drop_scales=drop32, taps=taps32)
+    m32 = {i: (taps32[f"dec{i}_z"] > 0).double() for i in mh}
+    flips = {f"dec{i}": {"hip": int(((mh[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum()),
+                         "fp32": int(((m32[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum())}
+             for i in mh}
+    del taps64, taps32
+    g64, _ = OE.train_step_grads(P, x64, d64, drop_scales=drop)
+    g32, _ = OE.train_step_grads(P32, x32, d64.float(), drop_scales=drop32)
+    plain = {k: {"hip": rel(hip[k], g64[k]), "fp32_restatement": rel(g32[k], g64[k])}
+             for k in g64}
+    del g64
+    g64h, _ = OE.train_step_grads(P, x64, d64, drop_scales=drop, relu_masks=mh)
+    g64f, _ = OE.train_step_grads(P, x64, d64, drop_scales=drop, relu_masks=m32)
+    return check_gradients(tag, hip, g64h, g32, structural_zero, g64_32=g64f,
+                           extra={"relu_flips_vs_fp64": flips, "plain_comparison": plain})
 
 
 def _residual_drop_blocks(eng):
@@ -239,14 +267,10 @@ def test_dropconnect_forward_and_gradients(cuda, fixed_schedules):
     assert rel(pred, pred_ref) < TOL
     loss_ref, dpred_ref = LM.hourglass_nll(y, pred_ref.numpy(), B, L)
     assert abs(loss.item() - loss_ref) / abs(loss_ref) < TOL
-    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
-    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
-    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
-                                 drop_scales={k: v.float() for k, v in drop.items()})
     nu = _nonuniform(drop)
     assert nu  # at least one block's branch is scaled differently across the batch
-    check_gradients("dropconnect128", {k: eng.grads[k] for k in g64}, g64, g32,
-                    lambda k: effnet_structural_zero(k, nu))
+    effnet_grads_flip_aware("dropconnect128", eng, weights, x, dpred_ref,
+                            lambda k: effnet_structural_zero(k, nu), drop=drop)
 
 
 # ------------------------------------------------------------------- cfg1: whole step
@@ -294,35 +318,10 @@ def test_cfg1_trainer_step_224(cuda, fixed_schedules):
     # passes its whole gradient in one realization and none in the other. One such pixel in a
     # channel whose beta gradient cancels to a small sum sets that tensor's max error
     # (tools/exp_relu_flips.py: the worst dec_bn{i}/beta channel holds a flipped pixel at every
-    # stage; the fp32 restatement flips 3-33 pixels per stage, HIP 1-13). Each implementation is
-    # therefore measured against the fp64 gradient along ITS OWN decoder ReLU branches; the
-    # plain comparison stays in the report.
-    drop32 = {k: v.float() for k, v in drop.items()}
-    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
-    taps32 = {}
-    with torch.no_grad():
-        OE.forward(P32, torch.tensor(x), drop_scales=drop32, taps=taps32)
-    m32 = {i: (taps32[f"dec{i}_z"] > 0).double() for i in range(len(eng.dec))}
-    mh = hip_decoder_relu_masks(eng, weights)
-    g64h, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop,
-                                  relu_masks=mh)
-    g64f, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop,
-                                  relu_masks=m32)
-    g64, _ = OE.train_step_grads(P, x64, torch.tensor(dpred_ref), drop_scales=drop)
-    g32, _ = OE.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(),
-                                 drop_scales=drop32)
+    # stage; the fp32 restatement flips 3-33 pixels per stage, HIP 1-13).
     nu = _nonuniform(drop)
-    with torch.no_grad():
-        taps64 = {}
-        OE.forward(P, x64, drop_scales=drop, taps=taps64)
-    flips = {f"dec{i}": {"hip": int(((mh[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum()),
-                         "fp32": int(((m32[i] > 0) != (taps64[f"dec{i}_z"] > 0)).sum())}
-             for i in range(len(eng.dec))}
-    plain = {k: {"hip": rel(eng.grads[k], g64[k]), "fp32_restatement": rel(g32[k], g64[k])}
-             for k in g64}
-    check_gradients("cfg1_224", {k: eng.grads[k] for k in g64}, g64h, g32,
-                    lambda k: effnet_structural_zero(k, nu), g64_32=g64f,
-                    extra={"relu_flips_vs_fp64": flips, "plain_comparison": plain})
+    effnet_grads_flip_aware("cfg1_224", eng, weights, x, dpred_ref,
+                            lambda k: effnet_structural_zero(k, nu), drop=drop)
     # Adam-AMSGrad (step 1) applied by the oracle to the step's own gradients
     z = np.zeros(params0.numel(), np.float32)
     p_ref, *_ = adam_amsgrad_step(params0.cpu().numpy(), eng.grads.buf.cpu().numpy(), z, z, z,
@@ -474,6 +473,10 @@ def test_batch32_bench_policy(cuda, model, bench_schedules):
     weights = eng.get_weights()
     eng.act["input"].copy_(torch.from_numpy(x))
     pred = eng.forward(training=True)
+    # ff_redweb: every ReLU branch the HIP forward took (its materialised ReLU outputs, read
+    # before the backward reuses any buffer), for the flip-aware gradient reference
+    mr = ({st: (eng.act[st] > 0).permute(0, 3, 1, 2).cpu() for st in OR.relu_sites()}
+          if model == "ff_redweb" else None)
     y = make_rankings(rng, B, H, H, R, L)
     loss, dpred, _ = K.listmle_fwd_bwd(pred, torch.from_numpy(y).to(cuda), B, R, L)
     eng.backward(dpred)
@@ -481,20 +484,29 @@ def test_batch32_bench_policy(cuda, model, bench_schedules):
     hip_taps = {n: mine(n).detach().cpu().double() for n in names}
     hip_pred, hip_loss = pred.detach().cpu().double(), loss.item()
     hip_grads = {k: eng.grads[k].detach().cpu() for k in O.trainable_names(weights)}
+    # ff_effnet: the decoder ReLU branches the HIP step took (flip-aware gradient reference, as
+    # in test_cfg1_trainer_step_224; the encoder's swish has no branch)
+    mh = hip_decoder_relu_masks(eng, weights) if model == "ff_effnet" else None
     del eng, pred, dpred
     torch.cuda.empty_cache()
     P = {k: torch.tensor(v, dtype=torch.float64) for k, v in weights.items()}
     taps = {}
+    b64, b32 = {}, {}  # ff_redweb: the fp64 / fp32 runs' own ReLU branches
+    kw64 = dict(kw, relu_branches=b64) if mr is not None else kw
     pred_ref, loss_ref, dpred_ref, g64 = _oracle_step(
-        O, P, torch.tensor(x, dtype=torch.float64), y, B, L, taps=taps, **kw)
+        O, P, torch.tensor(x, dtype=torch.float64), y, B, L, taps=taps, **kw64)
     ref = {n: taps[n].permute(0, 2, 3, 1) for n in names}
+    z64 = ({i: taps[f"dec{i}_z"] for i in range(len(mh))} if mh is not None else None)
     del taps
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
     taps32 = {}
     with torch.no_grad():
-        pred32 = O.forward(P32, torch.tensor(x), taps=taps32, **kw)
+        pred32 = O.forward(P32, torch.tensor(x), taps=taps32,
+                           **(dict(kw, relu_branches=b32) if mr is not None else kw))
     e32 = {n: rel(taps32[n].permute(0, 2, 3, 1), ref[n]) for n in names}
     e32["pred"] = rel(pred32, pred_ref)
+    m32 = ({i: (taps32[f"dec{i}_z"] > 0).double() for i in range(len(mh))}
+           if mh is not None else None)
     del taps32, pred32
     g32 = O.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred_ref).float(), **kw)[0]
     errs = {n: rel(hip_taps[n], ref[n]) for n in names}
@@ -506,4 +518,35 @@ def test_batch32_bench_policy(cuda, model, bench_schedules):
                                          "schedule_table_sha1": bench_schedules})
     print(errs, bars)
     assert all(errs[n] < bars[n] for n in errs), (errs, bars)
-    check_gradients(f"{model}_b32_auto_grads", hip_grads, g64, g32, zero)
+    if mr is not None:
+        # every ReLU of the ResNet encoder and the decoder, flip-aware as ff_effnet's decoder
+        x64 = torch.tensor(x, dtype=torch.float64)
+        dref = torch.tensor(dpred_ref, dtype=torch.float64)
+        flips = {st: {"hip": int((mr[st] != b64[st]).sum()), "fp32": int((b32[st] != b64[st]).sum())}
+                 for st in OR.relu_sites()}
+        tot = {"hip": sum(v["hip"] for v in flips.values()),
+               "fp32": sum(v["fp32"] for v in flips.values())}
+        plain = {k: {"hip": rel(hip_grads[k], g64[k]), "fp32_restatement": rel(g32[k], g64[k])}
+                 for k in g64}
+        del g64, b64
+        g64h = O.train_step_grads(P, x64, dref, relu_masks=mr, **kw)[0]
+        g64f = O.train_step_grads(P, x64, dref, relu_masks=b32, **kw)[0]
+        check_gradients(f"{model}_b32_auto_grads", hip_grads, g64h, g32, zero, g64_32=g64f,
+                        extra={"relu_flips_vs_fp64_total": tot, "relu_flips_vs_fp64": flips,
+                               "plain_comparison": plain})
+        return
+    # each implementation against the fp64 gradient along its own decoder ReLU branches, the
+    # strict bar for every tensor (no ill-conditioned exception); the plain comparison and the
+    # flip counts go to the report
+    x64 = torch.tensor(x, dtype=torch.float64)
+    dref = torch.tensor(dpred_ref, dtype=torch.float64)
+    flips = {f"dec{i}": {"hip": int(((mh[i] > 0) != (zr > 0)).sum()),
+                         "fp32": int(((m32[i] > 0) != (zr > 0)).sum())}
+             for i, zr in ((i, z64[i]) for i in range(len(mh)))}
+    plain = {k: {"hip": rel(hip_grads[k], g64[k]), "fp32_restatement": rel(g32[k], g64[k])}
+             for k in g64}
+    del g64
+    g64h = O.train_step_grads(P, x64, dref, relu_masks=mh)[0]
+    g64f = O.train_step_grads(P, x64, dref, relu_masks=m32)[0]
+    check_gradients(f"{model}_b32_auto_grads", hip_grads, g64h, g32, zero, g64_32=g64f,
+                    extra={"relu_flips_vs_fp64": flips, "plain_comparison": plain})
