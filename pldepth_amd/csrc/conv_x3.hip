@@ -163,6 +163,50 @@ __global__ __launch_bounds__(512) void conv_x3_patch_kernel(GemmConvParams p) {
 
   // ---- epilogue: tile row i = output pixel ox0 + i of row oy0 + wave (bias, routing, acc) ----
   const int oy = oy0 + wave;
+  // whole float4 column quads (N, split, leading dims in 4s, 16-byte bases): the wave's
+  // [32 px][BN] block through LDS (after every wave's last fragment read), out as 16-byte
+  // streaming stores of contiguous pixel runs — the conv_x3_kernel grid epilogue's form
+  const bool quads = (p.N & 3) == 0 && (p.split >= p.N || (p.split & 3) == 0) &&
+                     (p.ld1 & 3) == 0 && (reinterpret_cast<uintptr_t>(p.out1) & 15) == 0 &&
+                     (p.split >= p.N ||
+                      ((p.ld2 & 3) == 0 && (reinterpret_cast<uintptr_t>(p.out2) & 15) == 0));
+  if (quads) {
+    constexpr int LD = BN + 8;  // the two half-waves' rows (4 apart) 32 banks apart
+    static_assert(8 * 32 * LD * 4 <= S::BYTES, "epilogue staging fits the LDS");
+    __syncthreads();
+    float* buf = reinterpret_cast<float*>(smem) + wave * 32 * LD;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n0 + b * 32 + l32;
+      const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[b][r];
+        buf[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + b * 32 + l32] = v + bias;
+      }
+    }
+    if (oy >= p.oh) return;
+    constexpr int Q = BN / 4, IT = 32 * Q / 64;
+    float4 v[IT], prev[IT];
+    float* dst[IT];
+    bool ok[IT], accum[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {  // every destination read before any store (accumulate)
+      const int e = lane + 64 * i, px = e / Q, q = e - px * Q;
+      const int ox = ox0 + px, col = n0 + 4 * q;
+      v[i] = *reinterpret_cast<const float4*>(buf + px * LD + 4 * q);
+      ok[i] = ox < p.ow && col < p.N;
+      const long row = ((long)img * p.oh + oy) * p.ow + ox;
+      const bool first = col < p.split;
+      dst[i] = first ? p.out1 + row * p.ld1 + col : p.out2 + row * p.ld2 + (col - p.split);
+      accum[i] = ok[i] && (first ? p.acc1 : p.acc2);
+      prev[i] = accum[i] ? *reinterpret_cast<const float4*>(dst[i]) : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+      if (ok[i]) st_nt4(dst[i], accum[i] ? add4(prev[i], v[i]) : v[i]);
+    return;
+  }
   if (oy >= p.oh) return;
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
