@@ -130,6 +130,70 @@ __device__ __forceinline__ void acc_stats(const GemmConvParams& p, const floatx1
   }
 }
 
+// ---- staged epilogue (round 4): whole float4 column quads only (N, split, leading dims in 4s,
+// 16-byte bases), no split-K slab
+__device__ __forceinline__ bool staged_ok(const GemmConvParams& p) {
+  return p.zstride == 0 && (p.N & 3) == 0 && (p.split >= p.N || (p.split & 3) == 0) &&
+         (p.ld1 & 3) == 0 && (reinterpret_cast<uintptr_t>(p.out1) & 15) == 0 &&
+         (p.split >= p.N ||
+          ((p.ld2 & 3) == 0 && (reinterpret_cast<uintptr_t>(p.out2) & 15) == 0));
+}
+
+// A wave's TM x TN accumulators (+ bias, routing, accumulate) through its private LDS region
+// `buf` of 32 x (32 TN + 8) floats, one 32-row sub-tile at a time: written in the MFMA C layout,
+// read back as row-contiguous float4, stored as 16-byte streaming (nt) stores. The caller
+// guarantees that no other wave touches `buf` any more (after the K loop's last barrier).
+template <int TM, int TN>
+__device__ __forceinline__ void store_acc_staged(const GemmConvParams& p,
+                                                 const floatx16 (&acc)[TM][TN], int m_w, int n_w,
+                                                 int lane, float* buf) {
+  constexpr int WTN = TN * 32, LD = WTN + 8, Q = WTN / 4, IT = 32 * Q / 64;
+  static_assert(IT >= 1 && (32 * Q) % 64 == 0, "whole float4 passes");
+  const int h = lane >> 5, l32 = lane & 31;
+  float bias[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n_w + b * 32 + l32;
+    bias[b] = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[a][b][r];  // (through a scalar: see store_partial)
+        buf[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + b * 32 + l32] = v + bias[b];
+      }
+    // (one wave's LDS accesses complete in order: its reads see its writes, and the next
+    // sub-tile's writes follow these reads)
+    // in chunks of up to 4 quads per lane (registers: the wide tiles hold 128 accumulators)
+    constexpr int CH = IT < 4 ? IT : 4;
+    static_assert(IT % CH == 0, "whole chunks");
+#pragma unroll
+    for (int c = 0; c < IT; c += CH) {
+      float4 v[CH], prev[CH];
+      float* dst[CH];
+      bool ok[CH], accum[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {  // the chunk's destinations read before its stores
+        const int e = lane + 64 * (c + i), row = e / Q, q = e - row * Q;
+        const int grow = m_w + a * 32 + row, gcol = n_w + 4 * q;
+        v[i] = *reinterpret_cast<const float4*>(buf + row * LD + 4 * q);
+        ok[i] = grow < p.M && gcol < p.N;
+        const bool first = gcol < p.split;
+        dst[i] = first ? p.out1 + (long)grow * p.ld1 + gcol
+                       : p.out2 + (long)grow * p.ld2 + (gcol - p.split);
+        accum[i] = ok[i] && (first ? p.acc1 : p.acc2);
+        prev[i] = accum[i] ? *reinterpret_cast<const float4*>(dst[i]) : make_float4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        if (ok[i]) st_nt4(dst[i], accum[i] ? add4(prev[i], v[i]) : v[i]);
+    }
+  }
+}
+
 // ---- epilogue of a wave's TM x TN grid of 32x32 accumulators (C/D map of the 32x32 MFMA
 // forms: column = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)). m_w/n_w: the wave's first
 // output row/column. Split-K slabs (zstride > 0) get the raw sums; otherwise bias, two-way

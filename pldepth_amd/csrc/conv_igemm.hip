@@ -447,6 +447,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(GemmConvParams p) {
 
 #undef As
 #undef Bs
+  // the loop's last barrier has passed: the staging LDS is free, one region per wave
+  if constexpr (4 * 32 * (WTN + 8) <= 2 * (A_ELEMS + B_ELEMS)) {
+    if (staged_ok(p)) {
+      if (p.stats) acc_stats<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
+      store_acc_staged<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane,
+                               smem + wave * 32 * (WTN + 8));
+      return;
+    }
+  }
   store_acc<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
 }
 

@@ -458,57 +458,12 @@ __device__ __forceinline__ void store_partial(const GemmConvParams& p,
       }
 }
 
-// Grid-schedule epilogue through LDS: after the last K-step barrier the staging buffers are free
-// and each consumer wave owns a private region (no further barrier); the wave's sums + bias are
-// written in the MFMA C layout, read back as row-contiguous float4 and leave as 16-byte
-// streaming (nt) stores. For the short-K 1x1 convs the epilogue is a large share of the launch:
-// 192 -> 1152 at 14^2 x 32: 22.9 -> 18.3 us, the other 1x1 shapes -6 to -12 %, 3x3 decoder convs
-// unchanged (profiles/r04_epilogue_store_ab.txt: plain 16-B stores 20.0, write-through 19.1).
-// Overwrite without concat routing only (the accumulate / routed forms keep store_acc).
-template <int BM, int BN, int TM, int TN>
-struct X3EpiLds {
-  static constexpr int WTM = TM * 32, WTN = TN * 32, LD = WTN + 8;  // LD: half-waves 32 banks apart
-  static constexpr bool FITS = 4 * WTM * LD * 4 <= X3Smem<BM, BN>::BYTES;
-};
-__device__ __forceinline__ bool epi_lds_ok(const GemmConvParams& p) {
-  return p.zstride == 0 && !p.acc1 && !p.acc2 && p.split >= p.N && (p.N & 3) == 0 &&
-         (p.ld1 & 3) == 0 && ((reinterpret_cast<uintptr_t>(p.out1) & 15) == 0) &&
-         (long)p.M * p.ld1 * 4 < 0x7FFFFFF0L;
-}
-template <int BM, int BN, int TM, int TN>
-__device__ __forceinline__ void store_acc_lds(const GemmConvParams& p,
-                                              const floatx16 (&acc)[TM][TN], int m_w, int n_w,
-                                              int wave, int lane, unsigned char* smem) {
-  using E = X3EpiLds<BM, BN, TM, TN>;
-  float* buf = reinterpret_cast<float*>(smem) + wave * E::WTM * E::LD;
-  const int h = lane >> 5, l32 = lane & 31;
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int col = n_w + b * 32 + l32;
-    const float bias = (p.bias && col < p.N) ? p.bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = acc[a][b][r];
-        buf[(a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * E::LD + b * 32 + l32] = v + bias;
-      }
-  }
-  typedef unsigned u32x4e __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.out1, (long)p.M * p.ld1 * 4);
-  constexpr int Q = E::WTN / 4, IT = E::WTM * Q / 64;
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = lane + 64 * i, row = e / Q, c4 = e - row * Q;
-    const float4 v = *reinterpret_cast<const float4*>(buf + row * E::LD + 4 * c4);
-    const int grow = m_w + row, gcol = n_w + 4 * c4;
-    if (grow < p.M && gcol < p.N)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4e, v), rs,
-                                             (unsigned)(((long)grow * p.ld1 + gcol) * 4), 0,
-                                             2 /* nt */);
-  }
-}
-
+// Grid-schedule epilogue: after the last K-step barrier the staging buffers are free and each
+// consumer wave owns a private region, so its sums go out through store_acc_staged (LDS, 16-byte
+// streaming row stores) where the output takes whole float4 quads. The short-K 1x1 convs are
+// epilogue-heavy: 192 -> 1152 at 14^2 x 32: 22.9 -> 18.3 us, the other 1x1 shapes -6 to -12 %,
+// 3x3 decoder convs unchanged (profiles/r04_epilogue_store_ab.txt: plain 16-B stores 20.0,
+// write-through 19.1).
 template <int BM, int BN, int WM, int WN, int MODE, bool STREAM>
 __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned char* smem,
                                             int g_begin, int g_end, int nk, int wave, int lane,
@@ -604,11 +559,12 @@ __device__ __forceinline__ void x3_consumer(const GemmConvParams& p, unsigned ch
     }
   }
   if constexpr (!STREAM) {
-    if constexpr (X3EpiLds<BM, BN, TM, TN>::FITS) {
-      if (epi_lds_ok(p)) {
+    if constexpr (4 * 32 * (WTN + 8) * 4 <= S::BYTES) {
+      if (staged_ok(p)) {
         const int m_w = mb0 * BM + wm * WTM, n_w = nb0 * BN + wn * WTN;
         if (p.stats) acc_stats<TM, TN>(p, acc, m_w, n_w, lane);
-        store_acc_lds<BM, BN, TM, TN>(p, acc, m_w, n_w, wave, lane, smem);
+        store_acc_staged<TM, TN>(p, acc, m_w, n_w, lane,
+                                 reinterpret_cast<float*>(smem) + wave * 32 * (WTN + 8));
         return;
       }
     }
