@@ -86,7 +86,6 @@ struct FastDiv {
   __device__ __forceinline__ uint32_t mod(uint32_t n, uint32_t q) const { return n - q * d; }
 };
 
-// wave-level reductions (wave64)
 // 16-byte streaming store (nt): for outputs written once and read by a later kernel. Measured on
 // the BN apply (401408 x 144, back-to-back launches): 83.6 -> 66.9 us, 5.5 -> 6.9 TB/s
 // (profiles/r04_store_policy_ab.txt; write-through sc1 stores: no gain)
@@ -96,6 +95,7 @@ __device__ __forceinline__ void st_nt4(float* p, float4 v) {
   __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
 }
 
+// wave-level reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
