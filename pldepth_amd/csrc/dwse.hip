@@ -1017,8 +1017,19 @@ extern "C" int pld__bn_bwd_finish(const double* part, int nparts, const float* x
                                   int dx_accumulate, float* dgamma, float* dbeta,
                                   int param_accumulate, float* k12, hipStream_t st);
 
+// The BN-backward squeeze (img_chan_sum_kernel<true, true>) holds 136 VGPRs, i.e. 3 workgroups
+// per CU: se_rsplit's 1024-workgroup grid ran as 1.33 rounds of the 768 the chip holds at once.
+// One round of 768: 47.2 -> 44.1 us per launch, step +0.3 % in 4 of 4 alternating pairs; 1536
+// (two rounds) 47.8 us (profiles/r04_se_squeeze_grid_ab.txt)
+static int se_rsplit_bn(int n, int hw, int c) {
+  const int cy = std::max(1, (int)cdiv(c / 4, 256));
+  int rs = (int)std::max(1L, 768L / ((long)std::max(n, 1) * cy));
+  rs = std::min(rs, std::max(1, hw / 32));
+  return rs;
+}
+
 static size_t se_bn_ws_parts(int n, int hw, int c) {
-  return (size_t)n * se_rsplit(n, hw, c) * c;  // doubles per [img][split][c] plane
+  return (size_t)n * se_rsplit_bn(n, hw, c) * c;  // doubles per [img][split][c] plane
 }
 
 extern "C" size_t pld_se_bwd_bn_full_workspace_size(int n, int hw, int c, int cse) {
@@ -1042,7 +1053,7 @@ extern "C" int pld_se_bwd_bn_full(const float* dy, const float* x, const float* 
   PLD_CHECK_ARG(ws_bytes >= pld_se_bwd_bn_full_workspace_size(n, hw, c, cse),
                 "pld_se_bwd_bn_full: workspace too small");
   hipStream_t st = as_stream(stream);
-  const int rs = se_rsplit(n, hw, c);
+  const int rs = se_rsplit_bn(n, hw, c);
   const size_t np = se_bn_ws_parts(n, hw, c);
   double* part = (double*)ws;
   double* part4 = part + np;
