@@ -95,7 +95,8 @@ def profile_conv(trainer, lr, replays=None):
             args.tile = saved
             recs.append((kname, kind, mode_of[name], flops_of(args), bytes_of(args), e0, e1))
             if replays is not None:  # the same call again, for the graph-replayed timing
-                replays.append((kname, lambda: fn(args, *rest, **kw)))
+                replays.append((kname, flops_of(args), bytes_of(args),
+                                lambda: fn(args, *rest, **kw)))
             return r
         return w
 
@@ -263,21 +264,17 @@ def attach_traffic(roof, path, workload):
         roof["mfma_busy"] = t["mfma_busy"]
 
 
-def replay_dominant(trainer, replays, roof, reps=5):
-    """The dominant kernel's launches of one step (every conv call whose main kernel it is, same
-    arguments and schedules, in step order) captured into one hipGraph on the trainer's stream
-    and replayed `reps` times between HIP events on that stream: its duration without host launch
-    gaps, as the timed (graph-replayed) steps run it. Becomes the roofline's headline
-    achieved / frac; the eager per-call HIP-event figure stays beside it. The calls re-issue
-    the step's own convs after the timed region (their outputs are rewritten by the next step)."""
+HBM_PEAK_TBS = 8.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def _graph_ms(trainer, calls, reps):
+    """Capture `calls` (in order) into one hipGraph on the trainer's stream, replay it once to
+    warm, then `reps` times between HIP events on that stream: ms per replay."""
     from pldepth_amd import kernels as K
-    calls = [c for n, c in replays if n == roof["kernel"]]
-    if not calls:
-        return
     st = trainer.stream
     with torch.cuda.stream(st):
         g = K.Graph().capture(lambda: [c() for c in calls])
-        g.launch()  # warm
+        g.launch()
         st.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
@@ -285,20 +282,66 @@ def replay_dominant(trainer, replays, roof, reps=5):
             g.launch()
         e1.record(st)
         e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
     del g
+    return e0.elapsed_time(e1) / reps
+
+
+def replay_dominant(trainer, replays, roof, reps=5):
+    """The dominant kernel's launches of one step (every conv call whose main kernel it is, same
+    arguments and schedules, in step order) captured into one hipGraph on the trainer's stream
+    and replayed `reps` times between HIP events on that stream: its duration without host launch
+    gaps (roofline.graph_replay). The launches are also split by the bound their own shape sets
+    (roofline.by_bound): a launch whose algorithmic FLOP per byte lies below the ridge point
+    peak / 8 TB/s is HBM-bound and is scored in TB/s against the HBM peak, the rest against the
+    MFMA peak; each group is captured and timed on its own.
+    The replays re-issue the step's own convs after the timed region: their outputs are
+    rewritten by the next step, and the BN moving statistics that the statistics-gathering calls
+    update are saved before and restored after, so no later use sees replay state."""
+    calls = [(f, b, c) for n, f, b, c in replays if n == roof["kernel"]]
+    if not calls:
+        return
+    eng = trainer.engine
+    saved = eng.stats.buf.clone() if getattr(eng, "stats", None) is not None else None
+    try:
+        ms = _graph_ms(trainer, [c for _, _, c in calls], reps)
+        ridge = roof["peak"] * 1e12 / (HBM_PEAK_TBS * 1e12)  # FLOP per byte
+        groups = {"mfma": [x for x in calls if x[0] / x[1] >= ridge],
+                  "hbm": [x for x in calls if x[0] / x[1] < ridge]}
+        by_bound = {}
+        for bound, grp in groups.items():
+            if not grp:
+                continue
+            gms = _graph_ms(trainer, [c for _, _, c in grp], reps)
+            fl, by = sum(x[0] for x in grp), sum(x[1] for x in grp)
+            e = {"launches": len(grp), "ms_per_step": round(gms, 4),
+                 "flops_per_step": fl, "bytes_per_step": by}
+            if bound == "mfma":
+                ach = fl / (gms * 1e-3) / 1e12
+                e.update(achieved=round(ach, 3), peak=roof["peak"], unit="TFLOP/s",
+                         frac=round(ach / roof["peak"], 4))
+            else:
+                ach = by / (gms * 1e-3) / 1e12
+                e.update(achieved=round(ach, 3), peak=HBM_PEAK_TBS, unit="TB/s",
+                         frac=round(ach / HBM_PEAK_TBS, 4),
+                         note="algorithmic bytes (each operand once + the output) / time")
+            by_bound[bound] = e
+    finally:
+        if saved is not None:
+            eng.stats.buf.copy_(saved)
+            torch.cuda.synchronize()
     d = roof["dominant"]
     ach = d["flops_per_step"] / (ms * 1e-3) / 1e12
-    roof["eager"] = {"achieved": roof["achieved"], "frac": roof["frac"],
-                     "ms_per_step": d["ms_per_step"],
-                     "note": "HIP events around each conv call of one eager step"}
-    roof["achieved"] = round(ach, 3)
-    roof["frac"] = round(ach / roof["peak"], 4)
-    roof["timing"] = (f"graph replay: the {len(calls)} launches of {roof['kernel']} of one step "
-                      f"captured into one hipGraph, {reps} replays between HIP events on the "
-                      f"trainer's stream: {ms:.4f} ms per step")
-    d["graph_ms_per_step"] = round(ms, 4)
-    d["graph_avg_us"] = round(ms * 1e3 / len(calls), 2)
+    roof["graph_replay"] = {
+        "achieved": round(ach, 3), "frac": round(ach / roof["peak"], 4),
+        "ms_per_step": round(ms, 4), "avg_us": round(ms * 1e3 / len(calls), 2),
+        "timing": (f"the {len(calls)} launches of {roof['kernel']} of one step captured into one "
+                   f"hipGraph, {reps} replays between HIP events on the trainer's stream")}
+    roof["by_bound"] = by_bound
+    roof["by_bound_rule"] = (f"per launch: algorithmic FLOP/B >= ridge {ridge:.1f} "
+                             f"(= {roof['peak']} TFLOP/s / {HBM_PEAK_TBS} TB/s) -> mfma, else hbm")
+    # live headline (until a matching in-step rocprof profile replaces it: attach_graph_frac)
+    roof["achieved"], roof["frac"] = round(ach, 3), round(ach / roof["peak"], 4)
+    roof["headline"] = "graph_replay (live)"
 
 
 def attach_graph_frac(roof, path, workload):
@@ -319,14 +362,21 @@ def attach_graph_frac(roof, path, workload):
         return
     ach = d["flops_per_step"] / (t["ms_per_step"] * 1e-3) / 1e12
     roof["rocprof_step_replay"] = {"ms_per_step": t["ms_per_step"], "achieved": round(ach, 3),
-                            "frac": round(ach / roof["peak"], 4), "source": t["source"]}
+                                   "frac": round(ach / roof["peak"], 4), "source": t["source"]}
+    # the in-step figure (the timed steps' own execution, where the decoder
+    # weight gradients share the GPU on a side stream) is the headline; the live graph replay of
+    # the kernel's launches alone stays under graph_replay
+    roof["achieved"], roof["frac"] = roof["rocprof_step_replay"]["achieved"], \
+        roof["rocprof_step_replay"]["frac"]
+    roof["headline"] = "rocprof_step_replay (in-step, committed kernel trace at this workload)"
 
 
 def conv_roofline(recs, traffic_profile=None):
     """roofline object. Top level = the DOMINANT kernel (the conv kernel name with the largest
     summed time in the profiled step): achieved = its algorithmic FLOPs / its measured time (the
-    eager HIP-event time here; replay_dominant then replaces it with the graph-replayed time and
-    keeps this one under `eager`), peak = the MFMA peak of its arithmetic. `family` keeps the whole conv family (FLOP-weighted blend
+    eager HIP-event time here, kept under `eager`; replay_dominant replaces the headline with the
+    graph-replayed time, attach_graph_frac with the in-step rocprof time when a kernel trace of
+    this workload is committed), peak = the MFMA peak of its arithmetic. `family` keeps the whole conv family (FLOP-weighted blend
     of the families' peaks: the same FLOPs with every launch at its own family's peak). traffic
     (PMC HBM bytes) cannot be read inside this process: null here; the PMC pass of the same
     command is committed under profiles/ (traffic_profile) with the algorithmic bytes beside it."""
@@ -363,6 +413,10 @@ def conv_roofline(recs, traffic_profile=None):
         "kernel": dname,
         "achieved": round(d_ach, 3), "peak": round(d_peak, 1), "unit": "TFLOP/s",
         "frac": round(d_ach / d_peak, 4),
+        "headline": "eager (live)",
+        "eager": {"achieved": round(d_ach, 3), "frac": round(d_ach / d_peak, 4),
+                  "ms_per_step": dominant["ms_per_step"],
+                  "note": "HIP events around each conv call of one eager step"},
         "traffic": None,
         "traffic_profile": traffic_profile,
         "dominant": dominant,
@@ -638,11 +692,20 @@ def main():
     ap.add_argument("--tune", default="",
                     help="autotune the schedules by timing instead (each candidate timed alone "
                          "on a drained device) and write the table to this path")
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="seconds before a collective (or the rendezvous) that a rank never "
+                         "joins raises and ends the job with a non-zero status")
+    ap.add_argument("--debug-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    from pldepth_amd.dp import exit_on_failure
+    exit_on_failure(lambda: run(a, world), world)
+
+
+def run(a, world):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world}"
@@ -653,15 +716,17 @@ def main():
     pg = None
     if world > 1:
         import torch.distributed as dist
-        if a.backend == "nccl":  # RCCL over xGMI
-            dist.init_process_group("nccl", rank=rank, world_size=world,
-                                    device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(a.backend, rank=rank, world_size=world)
-        pg = dist.group.WORLD
+        from pldepth_amd import dp
+        # bounded: a rank that dies or never arrives ends the job (non-zero) within the timeout
+        # instead of leaving the others blocked in a collective
+        pg = dp.init_group(a.backend, rank, world, device=torch.device("cuda", dev),
+                           timeout_s=a.dist_timeout)
     # what the process group actually holds (the SCALE record shows RCCL saw N ranks)
     ranks_seen = dist.get_world_size() if world > 1 else 1
     backend_seen = str(dist.get_backend()) if world > 1 else None
+    if a.debug_fail_rank >= 0 and rank == a.debug_fail_rank:
+        log(f"--debug-fail-rank: rank {rank} exits before the first step")
+        os._exit(3)
 
     from pldepth_amd.build import LIB  # noqa: F401  (the built library must be present)
     from pldepth_amd import kernels as K
@@ -672,6 +737,8 @@ def main():
         n_sched, sha = K.use_schedule_table(path)
         sched = {"mode": "table", "table": os.path.relpath(path, ROOT), "sha1": sha,
                  "entries": n_sched}
+        if n_sched == 0:  # tuned on another arch / format: nothing taken
+            sched["mode"] = "default (table not applicable: 0 entries taken; cost-model schedules)"
 
     H = a.size
     B, L, R = a.batch, a.ranking_size, a.rankings_per_image
@@ -679,6 +746,14 @@ def main():
                              world, pg, graph=not a.no_graph)
     loss = tr.loss_value()
     value = world * B * a.steps / elapsed
+    dist_check = None
+    if world > 1:
+        # every replica applied the same all-reduced gradients: parameters equal bit for bit
+        from pldepth_amd import dp
+        same, sums = dp.replicas_identical(tr.engine.params.buf, pg)
+        dist_check = {"replicas_identical": same, "param_checksums": sums,
+                      "rccl_version": dp.rccl_version() if a.backend == "nccl" else None,
+                      "timeout_s": a.dist_timeout}
 
     # dominant conv kernel + conv family: algorithmic FLOPs / measured duration (HIP events on
     # the trainer's stream, one eager step)
@@ -724,6 +799,7 @@ def main():
                       "decoder": tr.engine.dec_math},
         "roofline": roof,
         "loss": loss,
+        "distributed": dist_check,
         "schedules": sched,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.no_loss_parity:

@@ -131,7 +131,10 @@ def _relu(x, site, masks=None, branches=None):
     branches another implementation took, for comparing arithmetic where a pre-activation lies
     within rounding of 0); branches: optional dict receiving {site: x > 0} (this run's own)."""
     if branches is not None:
-        branches[site] = (x > 0).detach()
+        if hasattr(branches, "record"):  # e.g. tests' FlipProbe: also sees the pre-activation
+            branches.record(site, x.detach())
+        else:
+            branches[site] = (x > 0).detach()
     if masks is not None and site in masks:
         return x * masks[site].to(x.dtype)
     return torch.relu(x)

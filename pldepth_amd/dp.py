@@ -56,4 +56,75 @@ def allreduce_bucket(flat, lo, hi, group=None):
     return dist.all_reduce(flat[lo:hi], group=group, async_op=True)
 
 
-__all__ = ["env_rank_world", "shard", "tensor_buckets", "allreduce_bucket"]
+def init_group(backend, rank, world, device=None, timeout_s=600):
+    """torch.distributed.init_process_group with a bound: the rendezvous and every later
+    collective raise after `timeout_s` instead of waiting forever on a rank that never arrives or
+    has died. "nccl" (RCCL) binds the group to `device` and turns on the watchdog's
+    asynchronous error handling, which aborts a collective stuck past the timeout; "gloo" raises
+    from the blocked call itself (or at once when a peer's socket closes)."""
+    import datetime
+    import torch.distributed as dist
+    td = datetime.timedelta(seconds=timeout_s)
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device, timeout=td)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=td)
+    return dist.group.WORLD
+
+
+def rccl_version():
+    """"major.minor.patch" of the RCCL library torch.distributed's nccl backend loaded (None when
+    torch has no nccl/RCCL build)."""
+    try:
+        import torch
+        v = torch.cuda.nccl.version()
+    except Exception:
+        return None
+    return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+
+
+def replica_checksum(buf):
+    """Two int64 checksums of a flat fp32 buffer's BIT patterns: their plain sum and a sum
+    weighted by position (1 + i mod 1021), so equal checksums mean equal buffers up to a
+    collision, not merely equal values in another order. Wraps modulo 2^64 (deterministic)."""
+    import torch
+    bits = buf.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    w = (torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1021) + 1
+    return torch.stack([bits.sum(), (bits * w).sum()])
+
+
+def replicas_identical(buf, group=None):
+    """After data-parallel steps every replica must hold the same parameters bit for bit (they
+    apply the same all-reduced gradient to the same weights). All-reduces MIN and MAX of each
+    rank's replica_checksum; returns (identical, {min, max})."""
+    import torch.distributed as dist
+    c = replica_checksum(buf)
+    lo, hi = c.clone(), c.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = lo.tolist(), hi.tolist()
+    return lo == hi, {"min": lo, "max": hi}
+
+
+def exit_on_failure(fn, world):
+    """Run fn(); in a multi-rank job an exception (a dead peer, a collective past its timeout)
+    ends THIS rank at once with a non-zero status instead of leaving it blocked in a later
+    collective or in process-group teardown; the launcher then stops the remaining ranks."""
+    import sys
+    import traceback
+    try:
+        return fn()
+    except BaseException as e:  # noqa: B902  (SystemExit included: keep its code)
+        if world <= 1:
+            raise
+        code = e.code if isinstance(e, SystemExit) and isinstance(e.code, int) and e.code else 1
+        rank = os.environ.get("RANK", "?")
+        print(f"[rank {rank}] failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        traceback.print_exc(file=sys.stderr)
+        sys.stderr.flush()
+        os._exit(code)
+
+
+__all__ = ["env_rank_world", "shard", "tensor_buckets", "allreduce_bucket", "init_group",
+           "rccl_version", "replica_checksum", "replicas_identical", "exit_on_failure"]

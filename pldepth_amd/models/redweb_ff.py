@@ -46,6 +46,8 @@ TAPS = ("conv2_block3_out", "conv3_block4_out", "conv4_block3_out", "conv5_block
 # per-product error sits far below the fp32 restatement's own gradient error, ~5e-2 per tensor
 # at batch 32).
 EXACT_STAGES_AUTO = ("conv2",)
+# Backward (dX / dW) convs kept exact under 'auto' (name prefixes; encoder or decoder).
+EXACT_BWD_AUTO = ()
 FFLS = [("ffl0", 256, 256, "conv4_block3_out"),
         ("ffl1", 128, 128, "conv3_block4_out"),
         ("ffl2", 64, 64, "conv2_block3_out")]
@@ -83,6 +85,10 @@ class RedWebFF:
         self.drop_connect = False  # no drop-connect in ResNet50 / ReDWeb
         # encoder convs (by Keras name prefix) kept in exact fp32 under the 'auto' policy
         self.exact_stages = EXACT_STAGES_AUTO
+        # name prefixes of convs (encoder or decoder) run exact fp32 in the backward / the
+        # forward under 'auto' besides exact_stages (RedWebFF._math)
+        self.exact_bwd = EXACT_BWD_AUTO
+        self.exact_fwd_extra = ()
         # backward: trainable convs' dW + db on a side stream (EffNetFF.overlap_wgrad)
         self.overlap_wgrad = int(os.environ.get("PLD_OVERLAP_WGRAD", "2"))
         # forward: each feature-fusion layer's left branch (conv0 + bn0 + block_left: it reads
@@ -258,10 +264,12 @@ class RedWebFF:
 
     # ------------------------------------------------------------------ forward
     def _math(self, conv, oh=None, ow=None, bwd=False):
+        if self.enc_math == "auto":
+            exact = self.exact_bwd if bwd else self.exact_stages + tuple(self.exact_fwd_extra)
+            if exact and conv.name.startswith(tuple(exact)):
+                return "fp32"
         if conv.trainable:
             return self.dec_math
-        if self.enc_math == "auto" and conv.name.startswith(self.exact_stages) and not bwd:
-            return "fp32"
         # "auto": per conv by the population its BN normalises over (kernels.encoder_math)
         return K.encoder_math(self.enc_math, self.B * (oh or 1) * (ow or 1),
                               getattr(self, "x3_min_population", None))

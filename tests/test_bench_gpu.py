@@ -43,6 +43,30 @@ def test_bench_world2_gloo_line(cuda):
     assert out["config"]["ranks_seen"] == 2
     assert out["value"] > 0 and out["steps"] == 3
     assert out["loss"] == out["loss"]  # finite
+    # the replicas' parameters agree bit for bit after the timed steps
+    d = out["distributed"]
+    assert d["replicas_identical"] is True, d
+    assert d["param_checksums"]["min"] == d["param_checksums"]["max"]
+    assert d["timeout_s"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_dead_rank_exits_nonzero(cuda):
+    """A rank that dies before the first step: the surviving rank's first collective fails (the
+    peer's socket closes, or the bounded timeout passes) and the job exits non-zero instead of
+    hanging (bench.py --dist-timeout, dp.exit_on_failure)."""
+    import time
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--backend", "gloo", "--size", "64", "--batch", "2", "--no-extra-configs",
+           "--no-cpu-baseline", "--dist-timeout", "60", "--debug-fail-rank", "1"]
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert time.time() - t0 < 250
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
 @pytest.mark.timeout(600)

@@ -9,6 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from pldepth_amd import dp
 from pldepth_amd.dp import allreduce_bucket, shard, tensor_buckets
 
 
@@ -108,3 +109,68 @@ def test_replica_gradients_average_matches_serial_shards():
     np.testing.assert_allclose(out[0][0], serial[::97].numpy(), rtol=1e-12, atol=1e-15)
     assert abs(out[0][1] - float(serial.sum())) <= 1e-9 * float(serial.abs().sum())
     np.testing.assert_array_equal(out[0][0], out[1][0])  # replicas stay bit-identical
+
+
+def _checksums(rank, world):
+    same = torch.linspace(-3, 3, 5000)
+    ok_same, sums = dp.replicas_identical(same)
+    other = same.clone()
+    if rank == 1:
+        other[4321] = torch.nextafter(other[4321], torch.tensor(10.0))  # one ulp on one rank
+    ok_other, _ = dp.replicas_identical(other)
+    swapped = same.clone()
+    if rank == 1:  # same values, two of them exchanged: the position weights catch it
+        swapped[[10, 20]] = swapped[[20, 10]]
+    ok_swapped, _ = dp.replicas_identical(swapped)
+    return ok_same, ok_other, ok_swapped, sums
+
+
+def test_replicas_identical_gloo():
+    out = _spawn(_checksums)
+    for r in (0, 1):
+        assert out[r][:3] == (True, False, False)
+        assert out[r][3]["min"] == out[r][3]["max"]
+
+
+def _dead_rank_job(rank, world, port, q):
+    """bench.py's multi-rank structure on gloo: bounded init, the run inside exit_on_failure,
+    rank 1 dying after the rendezvous, rank 0 then entering its first collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank))
+    torch.set_num_threads(1)
+    import time
+
+    def run():
+        dp.init_group("gloo", rank, world, timeout_s=20)
+        if rank == 1:
+            os._exit(3)
+        time.sleep(1.0)
+        dp.replicas_identical(torch.ones(100))  # the peer is gone: raises
+        q.put("unreachable")
+    dp.exit_on_failure(run, world)
+
+
+def test_dead_rank_makes_survivor_exit_nonzero():
+    import time
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    t0 = time.time()
+    ps = [ctx.Process(target=_dead_rank_job, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=120)
+    alive = [p.is_alive() for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert not any(alive), "a rank is still blocked after the timeout"
+    assert ps[1].exitcode == 3
+    assert ps[0].exitcode not in (0, None)
+    assert time.time() - t0 < 100
+    assert q.empty()
+
+
+def test_rccl_version_is_string_or_none():
+    v = dp.rccl_version()
+    assert v is None or (isinstance(v, str) and v.count(".") >= 1)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--cout", type=int, default=240)
     ap.add_argument("--math", default="bf16x3")
     ap.add_argument("--tile", type=int, default=-1, help="-1 = autotune")
+    ap.add_argument("--sched", default="", help="schedule by name (pld_conv_schedule_desc), "
+                    "e.g. x3split/128x128; overrides --tile")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--presplit", type=int, default=1)
     ap.add_argument("--acc", type=int, default=0, help="accumulate into the destination")
@@ -42,6 +44,10 @@ def main():
     pt = (a.k - 1) // 2
     args = K.conv_args(x1, x2, a.k, a.k, 1, pt, pt, a.h, a.w, a.cout, math=a.math)
     args.tile = a.tile
+    if a.sched:
+        idx = K._schedule_index(K.MATH[a.math], a.sched)
+        assert idx is not None, f"no schedule named {a.sched}"
+        args.tile = idx
     wn, wd = K.filter_to_native(w), K.filter_to_dgrad(w)
     if a.presplit and a.math == "bf16x3":
         if C % 8 == 0:
@@ -66,7 +72,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     fl = 2.0 * a.n * a.h * a.w * a.cout * a.k * a.k * C
     print(f"{a.mode} n{a.n} {a.h}x{a.w} c{a.c1}+{a.c2} k{a.k} cout{a.cout} {a.math} "
-          f"tile={args.tile}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+          f"tile={args.tile} {a.sched}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
 
 
 if __name__ == "__main__":
