@@ -977,12 +977,7 @@ extern "C" int pld__x3_launch(GemmConvParams* p, int mode, int splits, int cfg, 
   }
   hipStream_t st = as_stream(stream);
   if (mode == MODE_FWD) {
-    static const int dma_depth = [] {
-      const char* e = getenv("PLD_X3_DMA");
-      return e ? atoi(e) : 0;
-    }();
     if (sk_grid > 0) x3::launch_fwd_stream(*p, cfg, sk_grid, st);
-    else if (dma_depth >= 2 && x3::dma_fwd_ok(*p)) x3::launch_fwd_dma(*p, splits, cfg, dma_depth, st);
     else x3::launch_fwd_grid(*p, splits, cfg, st);
   } else {
     if (sk_grid > 0) x3::launch_wgrad_stream(*p, cfg, sk_grid, st);

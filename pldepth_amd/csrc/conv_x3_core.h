@@ -759,8 +759,5 @@ void launch_fwd_grid(GemmConvParams& p, int splits, int cfg, hipStream_t st);
 void launch_fwd_stream(GemmConvParams& p, int cfg, int sk_grid, hipStream_t st);
 void launch_wgrad_grid(GemmConvParams& p, int splits, int cfg, hipStream_t st);
 void launch_wgrad_stream(GemmConvParams& p, int cfg, int sk_grid, hipStream_t st);
-// conv_x3_dma.hip: the LDS-DMA form of the FWD-view grid schedule (depth = ring slots)
-bool dma_fwd_ok(const GemmConvParams& p);
-void launch_fwd_dma(GemmConvParams& p, int splits, int cfg, int depth, hipStream_t st);
 }  // namespace x3
 }  // namespace pld

@@ -36,6 +36,13 @@ VARIANTS = {
     "ffl_fwdbwd": (("ffl",), ("ffl",)),
     "conv5+ffl_down_fwdbwd": (("conv5",) + FFL_DOWN, ("conv5",) + FFL_DOWN),
     "dec_all_fwdbwd": (("ffl", "aol"), ("ffl", "aol")),
+    # the HIP backward fed the fp64 forward's dL/dpred (the fp32 restatement's input) instead of
+    # its own: separates the backward's arithmetic from the forward's error carried by dpred
+    "auto_dref": ((), ()),
+    # every conv of the step exact fp32 (the HIP exact-fp32 kernels): what an fp32 HIP path
+    # gives under the same comparison
+    "fp32_all": (("",), ("",)),
+    "fp32_all_dref": (("",), ("",)),
 }
 
 
@@ -85,9 +92,35 @@ def main():
     g32 = OR.train_step_grads(P32, torch.tensor(x), dref.float(), preprocessed=True)[0]
     g64f = OR.train_step_grads(P, x64, dref, preprocessed=True, relu_masks=b32)[0]
     e32 = {k: rel(g32[k], g64f[k]) for k in g64f if k not in zeros}
-    del g32, g64f
+    # the fp32 restatement end to end: its own forward's dL/dpred
+    with torch.no_grad():
+        pred32 = OR.forward(P32, torch.tensor(x), preprocessed=True)
+    _, dpred32 = LM.hourglass_nll(y, pred32.double().numpy(), B, L)
+    g32o = OR.train_step_grads(P32, torch.tensor(x), torch.tensor(dpred32).float(),
+                               preprocessed=True)[0]
+    e32_own = {k: rel(g32o[k], g64f[k]) for k in g64f if k not in zeros}
+    print("fp32 end-to-end within 1e-3:", sum(e <= TOL for e in e32_own.values()),
+          "dpred32 vs dref", rel(torch.tensor(dpred32), dref), flush=True)
+    del g32, g64f, g32o
+    # a second fp32 restatement: torch's native (im2col + sgemm) convolutions instead of oneDNN,
+    # i.e. the same semantics with another summation order, along its own ReLU branches
+    e32b = {}
+    if os.environ.get("PLD_EXP_FP32B", "1") == "1":
+        t1 = time.time()
+        with torch.backends.mkldnn.flags(enabled=False):
+            b32b = {}
+            with torch.no_grad():
+                OR.forward(P32, torch.tensor(x), preprocessed=True, relu_branches=b32b)
+            g32b = OR.train_step_grads(P32, torch.tensor(x), dref.float(), preprocessed=True)[0]
+        g64b = OR.train_step_grads(P, x64, dref, preprocessed=True, relu_masks=b32b)[0]
+        e32b = {k: rel(g32b[k], g64b[k]) for k in g64b if k not in zeros}
+        del g32b, g64b, b32b
+        both = sum(max(e32[k], e32b[k]) <= TOL for k in e32)
+        print(f"second fp32 restatement (no oneDNN): within 1e-3 {sum(e <= TOL for e in e32b.values())}"
+              f", both within {both} ({time.time() - t1:.0f} s)", flush=True)
     print(f"reference + fp32 restatement: {time.time() - t0:.0f} s", flush=True)
-    out = {"schedule_table": sha, "fp32_restatement": e32, "variants": {}}
+    out = {"schedule_table": sha, "fp32_restatement": e32, "fp32_restatement_own_dpred": e32_own,
+           "fp32_restatement_native_conv": e32b, "variants": {}}
     yt = torch.from_numpy(y).cuda()
     for v in names:
         fwd, bwd = VARIANTS[v]
@@ -97,6 +130,9 @@ def main():
         pred = eng.forward(training=True)
         mr = {st: (eng.act[st] > 0).permute(0, 3, 1, 2).cpu() for st in OR.relu_sites()}
         loss, dpred, _ = K.listmle_fwd_bwd(pred, yt, B, R, L)
+        e_dpred = rel(dpred, dref)
+        if v.endswith("_dref"):
+            dpred = dref.float().to(pred.device).reshape(dpred.shape)
         eng.backward(dpred)
         torch.cuda.synchronize()
         e_pred = rel(pred, pred_ref)
@@ -116,10 +152,10 @@ def main():
         loose_fail = {k: (eh[k], e32[k]) for k in e32 if e32[k] > TOL and eh[k] > 2 * e32[k]}
         worst = sorted(eh.items(), key=lambda kv: -kv[1] / max(e32[kv[0]], TOL))[:12]
         out["variants"][v] = {"exact_fwd": fwd, "exact_bwd": bwd, "ms_fwd_bwd": ms,
-                              "pred": e_pred, "within_1e-3": sum(e <= TOL for e in eh.values()),
+                              "pred": e_pred, "dpred": e_dpred, "within_1e-3": sum(e <= TOL for e in eh.values()),
                               "tensors": len(eh), "strict_fail": strict_fail,
                               "loose_fail": loose_fail, "worst": worst, "errors": eh}
-        print(f"{v}: {ms:.1f} ms  pred {e_pred:.2e}  within {out['variants'][v]['within_1e-3']}"
+        print(f"{v}: {ms:.1f} ms  pred {e_pred:.2e}  dpred {e_dpred:.2e}  within {out['variants'][v]['within_1e-3']}"
               f"/{len(eh)}  strict_fail {len(strict_fail)} {sorted(strict_fail.items())[:6]}  "
               f"loose_fail {len(loose_fail)}  (oracle {time.time() - t1:.0f} s)", flush=True)
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
