@@ -30,9 +30,10 @@ restatement lands within 1e-3 (HIP global rel-L2 8.6e-5); the ff_effnet tests he
 flip-aware reference with the strict 1e-3 bar and report the plain comparison and the flip counts
 beside it. The ff_redweb tests are flip-aware at all 86 ReLU sites; their per-tensor bar comes from
 TWO fp32 restatements (oneDNN and native convolutions): 1e-3 wherever both are within 5e-4, else
-twice the worse of the two (check_gradients' docstring has the measurements behind it). Every flip-aware test also checks
-that each HIP branch flip lies where the fp64 pre-activation is within rounding of 0
-(FLIP_MARGIN), so a wrong forward branch cannot hide in the flip-aware reference.
+SPREAD (2.5) x the worse of the two (check_gradients' docstring has the measurements behind it).
+Every flip-aware test also checks that each HIP branch flip lies where the fp64 pre-activation is
+within rounding of 0 (FLIP_MARGIN), so a wrong forward branch cannot hide in the flip-aware
+reference.
 """
 import json
 import os
@@ -103,8 +104,8 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
     second = (g32b, g64_32b): a second fp32 restatement (the same semantics with torch's native
     convolutions instead of oneDNN: another summation order) and its flip-aware fp64 reference.
     With it the per-tensor bar follows how well-conditioned the tensor is by BOTH fp32
-    restatements: 1e-3 wherever both are within 1e-3 / 2, else twice the larger of their errors
-    (1e-3 floor). Why (ff_redweb at batch 32, profiles/r05_redweb_parity_*): the two fp32
+    restatements: 1e-3 wherever both are within 1e-3 / 2, else SPREAD x the larger of their
+    errors (1e-3 floor). Why (ff_redweb at batch 32, profiles/r05_redweb_parity_*): the two fp32
     restatements' per-tensor errors differ by up to 2.35x (median 0.87) and disagree about 1e-3
     on 5 of 237 tensors; HIP's exact-fp32 path misses "1e-3 wherever the oneDNN restatement
     meets it" on 2-3 tensors, and running the conv5 stage or the FFL convs exact fp32 changes
@@ -120,7 +121,7 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
         else:
             e32b = rel(second[0][k], second[1][k])
             worst = max(e32, e32b)
-            bar = TOL if worst <= TOL / 2 else max(TOL, 2.0 * worst)
+            bar = TOL if worst <= TOL / 2 else max(TOL, SPREAD * worst)
             rows[k] = {"hip": e_hip, "fp32_restatement": e32, "fp32_restatement_native_conv": e32b,
                        "bar": bar}
         if e_hip > bar:
@@ -213,7 +214,14 @@ def hip_decoder_relu_masks(eng, weights):
 # site. The forward activations themselves agree with fp64 to ~1e-4 of their scale (taps,
 # test_batch32_bench_policy), so a flip further out means the forward took a wrong branch, which
 # the flip-aware gradient comparison would otherwise absorb.
-FLIP_MARGIN = 1e-2
+FLIP_MARGIN = 2e-3  # observed (round 5): <= 3e-5 ff_effnet, 4.1e-4 ff_redweb at batch 2
+
+# Per-tensor factor over the worse fp32 restatement where a tensor is not clearly
+# well-conditioned (check_gradients' `second`): two exact-fp32 restatements of ff_redweb at batch
+# 32 differ per tensor by up to 2.35x (profiles/r05_redweb_parity_two_fp32.json), so a HIP error
+# within 2.5x of the worse one is inside the spread of fp32 summation orders. (Observed HIP /
+# worse-fp32 ratio: median 1.08, largest 2.24 on one of 237 tensors, cfg3 batch 2.)
+SPREAD = 2.5
 
 
 def flip_margin(z64, hip_mask):

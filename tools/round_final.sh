@@ -7,6 +7,11 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 rc=0
+# progress marker for the GPU pool's silence watchdog (a parity test's fp64 oracle runs
+# several minutes without printing); every step below keeps its own time limit
+(while sleep 45; do date >> $O/heartbeat.txt; done) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 if [ "$2" != "--no-tests" ]; then
   export PLD_REPORT_DIR=$O/parity
   timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
