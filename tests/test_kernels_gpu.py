@@ -278,7 +278,11 @@ def test_conv_every_schedule(cuda, case, math):
     # dec_conv0-like 3x3 concat at 14 x 14 with long K (K = 11520): few tiles, stream-K cuts
     (2, 14, 14, 640, 640, 3, 336, True),
     # ragged everything: M, N and K tails, concat with a 16-channel chunk
-    (3, 11, 13, 48, 16, 3, 72, False)])
+    (3, 11, 13, 48, 16, 3, 72, False),
+    # more tiles than resident slots but whole tiles would leave the last round mostly empty
+    # (64x192 / 256x32: 576 tiles on 512 slots), long K (32 steps): balanced cut ranges, each
+    # workgroup a partial tile, whole tiles and another partial tile (round 5)
+    (2, 96, 96, 1024, 0, 1, 256, True)])
 def test_conv_tile_stream(cuda, case):
     """The bf16x3 tile-stream schedules (conv_x3_kernel STREAM + x3_stream_fixup_kernel): fwd
     (+bias, accumulate), dgrad into two concat destinations (accumulate on one), wgrad, and the

@@ -72,6 +72,22 @@ def main():
         print(f"window: {a.steps} steps, {len(rows) // per} dispatches/step, "
               f"wall {wall / 1e6:.3f} ms/step")
     out, total = stats(rows)
+    if a.marker:
+        # GPU busy time = union of all kernel intervals (the step runs on 2-3 streams); the rest
+        # of the wall is idle: kernel boundaries, launch gaps, dependency waits
+        busy, cur_s, cur_e = 0, None, None
+        for _, s0, e0 in sorted(rows, key=lambda r: r[1]):
+            if cur_e is None or s0 > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s0, e0
+            else:
+                cur_e = max(cur_e, e0)
+        busy += cur_e - cur_s
+        wall_ns = rows[-1][2] - rows[0][1]
+        print(f"gpu busy {busy / per / 1e6:.3f} ms/step (union of kernel intervals), idle "
+              f"{(wall_ns - busy) / per / 1e6:.3f} ms/step = {100.0 * (wall_ns - busy) / wall_ns:.1f} %"
+              f" of the wall")
     if a.csv:
         with open(a.csv, "w", newline="") as f:
             w = csv.writer(f)
