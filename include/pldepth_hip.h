@@ -273,6 +273,22 @@ int pld_bn_add_bwd(const float* x, const float* dy, int64_t rows, int c, const f
                    int act, float* dx, int dx_accumulate, float* dres, int dres_accumulate,
                    float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
 
+/* EfficientNet's residual MBConv output (keras efficientnet.block: project BN -> Dropout(
+ * drop_rate, noise_shape=(None, 1, 1, 1)) -> add([x, inputs]), the blocks pl_hourglass.py:48's
+ * EfficientNetB0 stacks): y = act(bn(x) * sample_scale[img] + res), img = row / hw, in one pass
+ * (the product and the sum rounded separately, as bn_apply + pld_residual_add); sample_scale
+ * from pld_dropconnect_scales, NULL = pld_bn_add_apply.  Backward: the BN(+act) backward of
+ * dy * sample_scale[img] (the scaled copy of dy never written); the residual branch's gradient
+ * is dy itself. */
+int pld_bn_scale_add_apply(const float* x, int64_t rows, int c, const float* mean,
+                           const float* invstd, const float* gamma, const float* beta,
+                           const float* sample_scale, int hw, const float* res, int act, float* y,
+                           void* stream);
+int pld_bn_bwd_scaled(const float* x, const float* dy, int64_t rows, int c, const float* mean,
+                      const float* invstd, const float* gamma, const float* beta, int act,
+                      const float* sample_scale, int hw, float* dx, int dx_accumulate,
+                      float* dgamma, float* dbeta, int param_accumulate, void* ws, void* stream);
+
 /* inference-mode BN (Keras BatchNormalization, training=False): scale = gamma/sqrt(mvar+eps),
  * shift = beta - mmean*scale, for pld_channel_affine_act / the conv prologue */
 int pld_bn_inference_coeffs(const float* gamma, const float* beta, const float* moving_mean,

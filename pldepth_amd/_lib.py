@@ -76,6 +76,9 @@ _SIGS = {
     "pld_pgemm_bn_act": (I32, [P, I64, I32, P, P, P, P, I32, P, I32, P, I32, P, I32, P]),
     "pld_pgemm_bn_bwd": (I32, [P, P, I64, I32, P, P, P, P, I32, P, P, I32, P, I32, P]),
     "pld_bn_add_apply": (I32, [P, I64, I32, P, P, P, P, P, I32, P, P]),
+    "pld_bn_scale_add_apply": (I32, [P, I64, I32, P, P, P, P, P, I32, P, I32, P, P]),
+    "pld_bn_bwd_scaled": (I32, [P, P, I64, I32, P, P, P, P, I32, P, I32, P, I32, P, P, I32, P,
+                                P]),
     "pld_bn_add_bwd": (I32, [P, P, I64, I32, P, P, P, P, P, I32, P, I32, P, I32, P, P, I32, P,
                              P]),
     "pld_maxpool2d_fwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P]),

@@ -37,6 +37,7 @@ struct RedParams {
   FastDiv dHW;
   double* partial;  // [C][gridDim.x][2]
   float* dz_out;    // BNBWD without gate/addn: also store dz = d(act input) (or NULL)
+  const float* sscale;  // BNBWD: dy scaled per image (drop-connect), [rows / hw], or NULL
 };
 
 template <int VW>
@@ -112,6 +113,11 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         for (int j = 0; j < RU; ++j) {
           ld<VW>(p.x + (r + j * rpi) * p.C + c0, xv[j]);
           ld<VW>(p.dy + (r + j * rpi) * p.C + c0, dv[j]);
+          if (p.sscale) {  // drop-connect: d(bn out) = dy * scale[img], rounded as its own product
+            const float sc = p.sscale[p.dHW.div((uint32_t)(r + j * rpi))];
+#pragma unroll
+            for (int u = 0; u < VW; ++u) dv[j][u] = __fmul_rn(dv[j][u], sc);
+          }
           if (p.res) {
             ld<VW>(p.res + (r + j * rpi) * p.C + c0, rv[j]);
           } else {
@@ -152,7 +158,12 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         float dv[VW];
         ld<VW>(p.dy + r * p.C + c0, dv);
         float g[VW], a[VW];
-        const long img = (p.gate || p.addn) ? (long)p.dHW.div((uint32_t)r) : 0;
+        const long img = (p.gate || p.addn || p.sscale) ? (long)p.dHW.div((uint32_t)r) : 0;
+        if (p.sscale) {
+          const float sc = p.sscale[img];
+#pragma unroll
+          for (int u = 0; u < VW; ++u) dv[u] = __fmul_rn(dv[u], sc);
+        }
 #pragma unroll
         for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
         if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
@@ -333,6 +344,7 @@ struct ApplyParams {
   FastDiv dHW;
   FastDiv dCV;
   float* y;
+  const float* sscale;  // per image (drop-connect): y = act(bn(x) * sscale[img] + res), or NULL
 };
 
 // The host sizes the grid so that its thread count is a multiple of C / VW: every thread's
@@ -365,11 +377,22 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
 #pragma unroll
       for (int u = 0; u < VW; ++u) xv[u] = xv[u] * mu[u] + is[u];
     }
-    if (p.res) {
+    if (p.sscale) {  // drop-connect scale of the BN output: fma with the residual, as residual_add
+      const float sc = p.sscale[p.dHW.div((uint32_t)p.dCV.div((uint32_t)e))];
+      if (p.res) {
+        float rv[VW];
+        ld<VW>(p.res + e * VW, rv);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) xv[u] = fmaf(xv[u], sc, rv[u]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < VW; ++u) xv[u] = __fmul_rn(xv[u], sc);
+      }
+    } else if (p.res) {
       float rv[VW];
       ld<VW>(p.res + e * VW, rv);
 #pragma unroll
-      for (int u = 0; u < VW; ++u) xv[u] += rv[u];
+      for (int u = 0; u < VW; ++u) xv[u] = __fadd_rn(xv[u], rv[u]);
     }
 #pragma unroll
     for (int u = 0; u < VW; ++u) g[u] = 1.f;
@@ -406,6 +429,7 @@ struct BwdApplyParams {
   const float* res;
   float* dres;  // receives dz = d(act input), the residual branch's gradient (or NULL)
   int dres_acc;
+  const float* sscale;  // dy scaled per image (drop-connect), or NULL
 };
 
 template <int VW, int ACT = -1>  // ACT >= 0: compile-time activation (as chan_reduce_kernel)
@@ -430,11 +454,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
     ld<VW>(p.dy + e * VW, dv);
 #pragma unroll
     for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
-    if (p.gate || p.addn) {
+    if (p.gate || p.addn || p.sscale) {
       const long r = (long)p.dCV.div((uint32_t)e);
       const long img = (long)p.dHW.div((uint32_t)r);
       if (p.gate) ld<VW>(p.gate + img * p.C + c0, g);
       if (p.addn) ld<VW>(p.addn + img * p.C + c0, a);
+      if (p.sscale) {
+        const float sc = p.sscale[img];
+#pragma unroll
+        for (int u = 0; u < VW; ++u) dv[u] = __fmul_rn(dv[u], sc);
+      }
     }
     float rv[VW];
 #pragma unroll
@@ -629,11 +658,12 @@ extern "C" int pld__bn_stats_finish(const double* part, int nparts, int64_t rows
 
 static int bn_apply_impl(const float* x, int64_t rows, int c, const float* mean,
                          const float* invstd, const float* gamma, const float* beta, int act,
-                         const float* gate, int hw, const float* res, float* y, void* stream) {
+                         const float* gate, int hw, const float* res, float* y, void* stream,
+                         const float* sscale = nullptr) {
   PLD_CHECK_ARG(x && y && mean && invstd && gamma && beta && rows > 0 && c > 0,
                 "pld_bn_apply: bad args");
   PLD_CHECK_ARG(!res || c % 4 != 0 || aligned16(res), "pld_bn_add_apply: res misaligned");
-  PLD_CHECK_ARG(!gate || hw > 0, "pld_bn_apply: gate needs hw > 0");
+  PLD_CHECK_ARG(!(gate || sscale) || hw > 0, "pld_bn_apply: gate / sample scale need hw > 0");
   ApplyParams p{};
   p.x = x;
   p.rows = rows;
@@ -645,6 +675,7 @@ static int bn_apply_impl(const float* x, int64_t rows, int c, const float* mean,
   p.act = act;
   p.gate = gate;
   p.res = res;
+  p.sscale = sscale;
   p.dHW = FastDiv((uint32_t)std::max(hw, 1));
   p.y = y;
   p.dCV = FastDiv((uint32_t)(c % 4 == 0 ? c / 4 : c));
@@ -669,6 +700,19 @@ extern "C" int pld_bn_add_apply(const float* x, int64_t rows, int c, const float
                                 const float* res, int act, float* y, void* stream) {
   PLD_CHECK_ARG(res, "pld_bn_add_apply: res is NULL");
   return bn_apply_impl(x, rows, c, mean, invstd, gamma, beta, act, nullptr, 0, res, y, stream);
+}
+
+// EfficientNet's residual MBConv output (Keras EfficientNetB0 block: Dropout(noise_shape =
+// (None, 1, 1, 1)) then add, applied to the project BN's output): y = act(bn(x) * sscale[img] +
+// res) in one pass, with the same roundings as bn_apply followed by residual_add (scale and
+// residual in one fma). sscale NULL = bn_add_apply.
+extern "C" int pld_bn_scale_add_apply(const float* x, int64_t rows, int c, const float* mean,
+                                      const float* invstd, const float* gamma, const float* beta,
+                                      const float* sample_scale, int hw, const float* res, int act,
+                                      float* y, void* stream) {
+  PLD_CHECK_ARG(res, "pld_bn_scale_add_apply: res is NULL");
+  return bn_apply_impl(x, rows, c, mean, invstd, gamma, beta, act, nullptr, hw, res, y, stream,
+                       sample_scale);
 }
 
 extern "C" int pld_channel_affine_act(const float* x, int64_t rows, int c, const float* scale,
@@ -699,18 +743,19 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
                          const float* gamma, const float* beta, int act, const float* gate,
                          const float* addn, FastDiv dHW, const float* res, float* dx,
                          int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
-                         float* dbeta, int param_accumulate, float* k12, hipStream_t st);
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st,
+                         const float* sscale = nullptr);
 
 static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, const float* mean,
                        const float* invstd, const float* gamma, const float* beta, int act,
                        const float* gate, const float* addn, int hw, const float* res,
                        float* dx, int dx_accumulate, float* dres, int dres_accumulate,
                        float* dgamma, float* dbeta, int param_accumulate, void* ws,
-                       void* stream) {
+                       void* stream, const float* sscale = nullptr) {
   PLD_CHECK_ARG(x && dy && mean && invstd && gamma && beta && ws && rows > 0 && c > 0,
                 "pld_bn_bwd: bad args");
   PLD_CHECK_ARG(rows < (1L << 31), "pld_bn_bwd: too many rows");
-  PLD_CHECK_ARG(!(gate || addn) || hw > 0, "pld_bn_bwd: gate/addn need hw > 0");
+  PLD_CHECK_ARG(!(gate || addn || sscale) || hw > 0, "pld_bn_bwd: gate/addn/scale need hw > 0");
   hipStream_t st = as_stream(stream);
   RedParams p{};
   p.x = x;
@@ -725,6 +770,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
   p.gate = gate;
   p.addn = addn;
   p.res = res;
+  p.sscale = sscale;
   p.dHW = FastDiv((uint32_t)std::max(hw, 1));
   p.partial = (double*)ws;
   // Residual form with an activation and a fresh dres: the reduction pass stores dz (= dres, the
@@ -732,7 +778,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
   // of (x, dy, res): 28 instead of 32 bytes per element. Without an activation dz = dy and the
   // mask needs no residual.
   const bool dz_pass = res && act != ACT_NONE && dres && !dres_accumulate && !gate && !addn &&
-                       dres != dy && dres != x && dres != res;
+                       !sscale && dres != dy && dres != x && dres != res;
   if (res && act == ACT_NONE) p.res = nullptr;
   if (dz_pass) p.dz_out = dres;
   int rc = launch_reduce(RED_BNBWD, p, st);
@@ -746,7 +792,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t rows, int c, con
                          dbeta, param_accumulate, k12, st);
   return bn_bwd_finish(p.partial, nbx, x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn,
                        p.dHW, p.res, dx, dx_accumulate, dres, dres_accumulate, dgamma, dbeta,
-                       param_accumulate, k12, st);
+                       param_accumulate, k12, st, sscale);
 }
 
 // finalize (dgamma, dbeta, k1 = mean dz, k2 = mean dz xhat from nbx channel-major partials) +
@@ -756,7 +802,8 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
                          const float* gamma, const float* beta, int act, const float* gate,
                          const float* addn, FastDiv dHW, const float* res, float* dx,
                          int dx_accumulate, float* dres, int dres_accumulate, float* dgamma,
-                         float* dbeta, int param_accumulate, float* k12, hipStream_t st) {
+                         float* dbeta, int param_accumulate, float* k12, hipStream_t st,
+                         const float* sscale) {
   bnbwd_finalize_kernel<<<c, 256, 0, st>>>(part, nbx, c, rows, dgamma, dbeta,
                                                        param_accumulate, k12);
   int rc = check_launch("bnbwd_finalize_kernel");
@@ -781,6 +828,7 @@ static int bn_bwd_finish(const double* part, int nbx, const float* x, const floa
   q.res = res;
   q.dres = dres;
   q.dres_acc = dres_accumulate;
+  q.sscale = sscale;
   if (c % 4 == 0) {
     const unsigned g = ew_grid_c(rows * c / 4, c / 4);
     if (act == ACT_NONE) bn_bwd_apply_kernel<4, ACT_NONE><<<g, 256, 0, st>>>(q);
@@ -848,6 +896,19 @@ extern "C" int pld_bn_bwd(const float* x, const float* dy, int64_t rows, int c, 
                           void* ws, void* stream) {
   return bn_bwd_impl(x, dy, rows, c, mean, invstd, gamma, beta, act, gate, addn, hw, nullptr,
                      dx, dx_accumulate, nullptr, 0, dgamma, dbeta, param_accumulate, ws, stream);
+}
+
+// the backward of pld_bn_scale_add_apply's BN branch: BN(+act) backward of dy * sscale[img]
+// (the drop-connect scale folded into both passes instead of a scaled copy of dy)
+extern "C" int pld_bn_bwd_scaled(const float* x, const float* dy, int64_t rows, int c,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, const float* sample_scale, int hw,
+                                 float* dx, int dx_accumulate, float* dgamma, float* dbeta,
+                                 int param_accumulate, void* ws, void* stream) {
+  PLD_CHECK_ARG(sample_scale, "pld_bn_bwd_scaled: sample_scale is NULL");
+  return bn_bwd_impl(x, dy, rows, c, mean, invstd, gamma, beta, act, nullptr, nullptr, hw,
+                     nullptr, dx, dx_accumulate, nullptr, 0, dgamma, dbeta, param_accumulate, ws,
+                     stream, sample_scale);
 }
 
 extern "C" int pld_bn_add_bwd(const float* x, const float* dy, int64_t rows, int c,

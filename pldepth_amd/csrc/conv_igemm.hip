@@ -943,10 +943,10 @@ static void x3_fwd_plan(long M, long N, long K, long ktiles, int tile, int& cfg,
 
 // tile-stream plan: T tiles of nk K-steps on occ resident workgroups per CU. As many tiles as
 // resident slots or more: whole tiles per workgroup, balanced (the pipeline runs on from tile to
-// tile) — unless whole tiles leave the last round mostly empty (T / slots = 4.2 runs 5 rounds:
-// 16 % of the launch idle), in which case the (tile, K-step) space is cut evenly over the slots
-// (round 5); fewer tiles than slots: the space cut evenly, >= 16 K-steps each (stream-K: cut
-// tiles are summed by the fixup kernel). Returns the grid; sets p.sk_*.
+// tile); fewer: the (tile, K-step) space cut evenly over the slots, >= 16 K-steps each
+// (stream-K: cut tiles are summed by the fixup kernel). Returns the grid; sets p.sk_*.
+// (Round 5 measured cutting evenly also when whole tiles quantise badly — T / slots = 4.2 runs 5
+// rounds — on the decoder dgrads: no faster than the grid, profiles/r05_stream_sweep.txt.)
 static int x3_stream_plan(GemmConvParams& p, int cfg, long ktiles) {
   int bm, bn, tm, tn, occ;
   pld__x3_cfg_dims(cfg, &bm, &bn, &tm, &tn, &occ);
@@ -956,14 +956,10 @@ static int x3_stream_plan(GemmConvParams& p, int cfg, long ktiles) {
   p.sk_tiles = (int)tiles;
   p.sk_nnb = (int)cdiv(p.N, bn);
   long G;
-  const long per = cdiv(tiles, slots);
-  // (a cut costs a slab round trip and a fixup: only long-K tiles, >= 32 K-steps, are cut)
-  if (tiles >= slots && ((double)tiles / (double)(per * slots) >= 0.9 || ktiles < 32)) {
+  if (tiles >= slots) {
+    const long per = cdiv(tiles, slots);
     G = cdiv(tiles, per);
     p.sk_align = 1;
-  } else if (tiles >= slots) {  // balanced cut ranges: every slot busy to the end
-    G = slots;
-    p.sk_align = 0;
   } else {
     G = std::min<long>(slots, std::max<long>(tiles, tiles * ktiles / 16));
     p.sk_align = (G == tiles) ? 1 : 0;

@@ -268,9 +268,8 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long)gridDim.x * blockDim.x) {
     const float s = sc ? sc[e / per] : 1.f;
-    float v = a[e] * s;
-    if (b) v += b[e];
-    if (acc) v += y[e];
+    float v = b ? fmaf(a[e], s, b[e]) : __fmul_rn(a[e], s);  // one rounding, as bn_scale_add_apply
+    if (acc) v = __fadd_rn(v, y[e]);
     y[e] = v;
   }
 }
@@ -286,10 +285,12 @@ __global__ __launch_bounds__(256) void residual4_kernel(const float4* __restrict
        e += gridDim.x * blockDim.x) {
     const float s = sc ? sc[dPer4.div(e)] : 1.f;
     const float4 u = a[e];
-    float4 v = make_float4(u.x * s, u.y * s, u.z * s, u.w * s);
-    if (b) {
+    float4 v;
+    if (b) {  // fma: one rounding, as pld_bn_scale_add_apply
       const float4 w = b[e];
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      v = make_float4(fmaf(u.x, s, w.x), fmaf(u.y, s, w.y), fmaf(u.z, s, w.z), fmaf(u.w, s, w.w));
+    } else {
+      v = make_float4(__fmul_rn(u.x, s), __fmul_rn(u.y, s), __fmul_rn(u.z, s), __fmul_rn(u.w, s));
     }
     y[e] = v;
   }

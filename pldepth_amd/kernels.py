@@ -624,6 +624,23 @@ def bn_add_apply(x, rows, c, mean, invstd, gamma, beta, res, act, y):
                            ptr(res), ACT[act], ptr(y), stream())
 
 
+def bn_scale_add_apply(x, rows, c, mean, invstd, gamma, beta, sample_scale, hw, res, act, y):
+    """y = act(bn(x) * sample_scale[row // hw] + res) (pld_bn_scale_add_apply; sample_scale None:
+    bn_add_apply)."""
+    lib().pld_bn_scale_add_apply(ptr(x), rows, c, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                                 ptr(sample_scale), hw, ptr(res), ACT[act], ptr(y), stream())
+
+
+def bn_bwd_scaled(x, dy, rows, c, mean, invstd, gamma, beta, act, sample_scale, hw, dx, dgamma,
+                  dbeta, dx_accumulate=False, param_accumulate=False):
+    """bn_bwd of dy * sample_scale[row // hw] (pld_bn_bwd_scaled)."""
+    ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")
+    lib().pld_bn_bwd_scaled(ptr(x), ptr(dy), rows, c, ptr(mean), ptr(invstd), ptr(gamma),
+                            ptr(beta), ACT[act], ptr(sample_scale), hw, ptr(dx),
+                            int(dx_accumulate), ptr(dgamma), ptr(dbeta), int(param_accumulate),
+                            ptr(ws), stream())
+
+
 def bn_add_bwd(x, dy, rows, c, mean, invstd, gamma, beta, res, act, dx, dres, dgamma, dbeta,
                dx_accumulate=False, dres_accumulate=False, param_accumulate=False):
     ws = workspace(lib().pld_channel_reduce_workspace_size(rows, c), "reduce")

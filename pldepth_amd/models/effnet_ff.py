@@ -285,7 +285,6 @@ class EffNetFF:
             blk["gate"] = torch.empty(B, cexp, device=dev)
             blk["addn"] = torch.empty(B, cexp, device=dev)
             blk["drop"] = torch.ones(B, device=dev)
-            blk["dbn"] = torch.empty(B, oh, ow, cout, device=dev) if blk["residual"] else None
             # thin-N 1x1 convs with their neighbouring elementwise op folded in (pgemm.hip):
             # the project conv over BN + swish + SE gate, the expand dgrad over the BN backward
             blk["fused_project"] = self.fuse_pgemm and K.pgemm_pays(cexp, cout)
@@ -469,14 +468,19 @@ class EffNetFF:
                                            blk["cout"], math=self._em(oh, ow)),
                                blk["project"].w_nat, None, A[n + "project_pre"], rows, training)
         out = A[n + "output"]
-        pbn.apply(A[n + "project_pre"], rows, "none", out, training)
-        if blk["residual"]:
+        if blk["residual"] and training:
+            # project BN -> drop-connect -> + block input in one pass (pld_bn_scale_add_apply)
             drop = None
-            if training and self.drop_connect and blk["rate"] > 0:
+            if self.drop_connect and blk["rate"] > 0:
                 K.dropconnect_scales(blk["drop"], blk["rate"], self.seed, step, li,
                                      getattr(self, "_img_off", 0))
                 drop = blk["drop"]
-            K.residual_add(out, drop, x, out)
+            K.bn_scale_add_apply(A[n + "project_pre"], rows, blk["cout"], pbn.mean, pbn.invstd,
+                                 pbn.gamma, pbn.beta, drop, oh * ow, x, "none", out)
+            return out
+        pbn.apply(A[n + "project_pre"], rows, "none", out, training)
+        if blk["residual"]:
+            K.residual_add(out, None, x, out)
         return out
 
     def _conv_bn(self, args, w_nat, bias, out, bn, rows, training):
@@ -605,17 +609,17 @@ class EffNetFF:
         h, w, oh, ow = blk["h"], blk["w"], blk["oh"], blk["ow"]
         rows = B * oh * ow
         gy = G[n + "output"]
-        if blk["residual"]:
-            drop = blk["drop"] if (self.drop_connect and blk["rate"] > 0) else None
-            if drop is not None:
-                K.scale_per_sample(gy, drop, blk["dbn"])
-                gbn = blk["dbn"]
-            else:
-                gbn = gy
-        else:
-            gbn = gy
+        drop = None
+        if blk["residual"] and self.drop_connect and blk["rate"] > 0:
+            drop = blk["drop"]
         gp = self._gpre_buf(A[n + "project_pre"].shape)
-        blk["project_bn"].bwd(A[n + "project_pre"], gbn, rows, "none", gp)
+        pbn = blk["project_bn"]
+        if drop is not None:  # the BN backward of dy * drop (no scaled copy of dy)
+            K.bn_bwd_scaled(A[n + "project_pre"], gy, rows, pbn.c, pbn.mean, pbn.invstd,
+                            pbn.gamma, pbn.beta, "none", drop, oh * ow, gp, pbn.dgamma,
+                            pbn.dbeta)
+        else:
+            pbn.bwd(A[n + "project_pre"], gy, rows, "none", gp)
         gse = G[n + "se_excite"]
         K.conv2d_dgrad(K.conv_args(A[n + "se_excite"], None, 1, 1, 1, 0, 0, oh, ow, blk["cout"],
                                    math=self._em(oh, ow)),

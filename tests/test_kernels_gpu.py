@@ -279,9 +279,8 @@ def test_conv_every_schedule(cuda, case, math):
     (2, 14, 14, 640, 640, 3, 336, True),
     # ragged everything: M, N and K tails, concat with a 16-channel chunk
     (3, 11, 13, 48, 16, 3, 72, False),
-    # more tiles than resident slots but whole tiles would leave the last round mostly empty
-    # (64x192 / 256x32: 576 tiles on 512 slots), long K (32 steps): balanced cut ranges, each
-    # workgroup a partial tile, whole tiles and another partial tile (round 5)
+    # long K (32 steps) with more tiles than resident slots on some tiles (64x192 / 256x32: 576
+    # tiles on 512 slots, two whole tiles per workgroup) and fewer on others (stream-K cuts)
     (2, 96, 96, 1024, 0, 1, 256, True)])
 def test_conv_tile_stream(cuda, case):
     """The bf16x3 tile-stream schedules (conv_x3_kernel STREAM + x3_stream_fixup_kernel): fwd
@@ -1019,6 +1018,41 @@ def test_bn_add_forward_backward(cuda, rows, c, act, dres_acc):
     assert rel_err(dres - base, rr.grad) < 1e-5
     assert rel_err(dg, gr.grad) < 1e-5
     assert rel_err(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n,hw,c", [(4, 49, 40), (3, 25, 6), (2, 196, 112), (5, 9, 3)])
+def test_bn_scale_add_fused_matches_unfused(cuda, n, hw, c):
+    """The EfficientNet residual block output (project BN, drop-connect scale, residual add) in
+    one pass (pld_bn_scale_add_apply) and its BN backward with the scale folded in
+    (pld_bn_bwd_scaled) are bit-identical to bn_apply + residual_add and scale_per_sample +
+    bn_bwd; the float4 (c % 4 == 0) and scalar paths, the row-blocked and general reductions."""
+    torch.manual_seed(n * 1000 + hw + c)
+    rows = n * hw
+    x = dev(torch.randn(rows, c) * 2 + 0.5, cuda)
+    res = dev(torch.randn(rows, c), cuda)
+    dy = dev(torch.randn(rows, c), cuda)
+    gam = dev(torch.rand(c) + 0.5, cuda)
+    bet = dev(torch.randn(c), cuda)
+    sc = dev(torch.tensor([0.0, 1.25, 1.25, 1.25, 0.0][:n]), cuda)
+    gm, gi = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_stats(x, rows, c, gm, gi)
+    y_un = torch.empty_like(x)
+    K.bn_apply(x, rows, c, gm, gi, gam, bet, "none", y_un)
+    K.residual_add(y_un.view(n, hw, c), sc, res.view(n, hw, c), y_un.view(n, hw, c))
+    y = torch.empty_like(x)
+    K.bn_scale_add_apply(x, rows, c, gm, gi, gam, bet, sc, hw, res, "none", y)
+    ds = torch.empty_like(x)
+    K.scale_per_sample(dy.view(n, hw, c), sc, ds.view(n, hw, c))
+    dx_un, dg_un, db_un = torch.empty_like(x), torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd(x, ds, rows, c, gm, gi, gam, bet, "none", dx_un, dg_un, db_un)
+    dx, dg, db = torch.full_like(x, 7.0), torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    K.bn_bwd_scaled(x, dy, rows, c, gm, gi, gam, bet, "none", sc, hw, dx, dg, db)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_un)
+    assert torch.equal(dx, dx_un)
+    assert torch.equal(dg, dg_un) and torch.equal(db, db_un)
+    # a dropped image passes only its residual
+    assert torch.equal(y.view(n, hw, c)[0], res.view(n, hw, c)[0])
 
 
 # thin 1x1 convs (csrc/thin.hip): K <= 48, VALU with the filter in SGPRs; ragged
