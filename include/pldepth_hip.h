@@ -376,6 +376,12 @@ int pld_dropconnect_scales(float* scales, int n, float rate, uint64_t seed, uint
 int pld_dropconnect_scales_dev(float* scales, int n, float rate, uint64_t seed,
                                const int64_t* step_dev, int layer, int image_offset,
                                void* stream);
+/* The same keep factors for nl <= 32 layers in one launch: scales[s * n + i] = the factor of
+ * layer layers[s] at rate rates[s] (host arrays); the step from step_dev when it is non-NULL
+ * (graph replay), else from step. */
+int pld_dropconnect_scales_multi(float* scales, int n, int nl, const float* rates,
+                                 const int* layers, uint64_t seed, uint64_t step,
+                                 const int64_t* step_dev, int image_offset, void* stream);
 /* y[i] = x[i] * sample_scale[img] (+ y[i] when accumulate) */
 int pld_scale_per_sample(const float* x, const float* sample_scale, int n, int64_t elems_per_img,
                          float* y, int accumulate, void* stream);

@@ -46,6 +46,7 @@ _SIGS = {
     "pld_set_scalar_f32": (I32, [P, F32, P]),
     "pld_sampler_draw_dev": (I32, [P, I32, I32, I32, U64, P, I32, P, P]),
     "pld_dropconnect_scales_dev": (I32, [P, I32, F32, U64, P, I32, I32, P]),
+    "pld_dropconnect_scales_multi": (I32, [P, I32, I32, P, P, U64, U64, P, I32, P]),
     "pld_conv2d_fwd": (I32, [C.POINTER(ConvArgs), P, P, P, I32, P]),
     "pld_conv2d_dgrad": (I32, [C.POINTER(ConvArgs), P, P, P, I32, P, I32, P]),
     "pld_conv2d_wgrad_workspace_size": (SZ, [C.POINTER(ConvArgs)]),

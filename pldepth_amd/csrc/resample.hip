@@ -296,13 +296,9 @@ __global__ __launch_bounds__(256) void residual4_kernel(const float4* __restrict
   }
 }
 
-__global__ void dropconnect_kernel(float* __restrict__ sc, int n, float rate, uint64_t seed,
-                                   uint64_t step_arg, const int64_t* __restrict__ step_dev,
-                                   int layer, int off) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t step = step_dev ? (uint64_t)step_dev[0] : step_arg;
-  uint4 c = make_uint4((uint32_t)layer, (uint32_t)(off + i), (uint32_t)step,
+__device__ __forceinline__ float dropconnect_scale(float rate, uint64_t seed, uint64_t step,
+                                                   int layer, int img) {
+  uint4 c = make_uint4((uint32_t)layer, (uint32_t)img, (uint32_t)step,
                        (uint32_t)(step >> 32) ^ 0x5D0Cu);
   uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
 #pragma unroll
@@ -314,7 +310,32 @@ __global__ void dropconnect_kernel(float* __restrict__ sc, int n, float rate, ui
     k.y += 0xBB67AE85u;
   }
   const float u = (float)(c.x >> 8) * (1.0f / 16777216.0f);  // [0, 1)
-  sc[i] = (u >= rate) ? 1.0f / (1.0f - rate) : 0.0f;
+  return (u >= rate) ? 1.0f / (1.0f - rate) : 0.0f;
+}
+
+__global__ void dropconnect_kernel(float* __restrict__ sc, int n, float rate, uint64_t seed,
+                                   uint64_t step_arg, const int64_t* __restrict__ step_dev,
+                                   int layer, int off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t step = step_dev ? (uint64_t)step_dev[0] : step_arg;
+  sc[i] = dropconnect_scale(rate, seed, step, layer, off + i);
+}
+
+// every drop-connect layer of one step in one launch: blockIdx.y = layer slot
+constexpr int DC_MAX_LAYERS = 32;
+struct DcLayers {
+  float rate[DC_MAX_LAYERS];
+  int layer[DC_MAX_LAYERS];
+};
+__global__ void dropconnect_multi_kernel(float* __restrict__ sc, int n, DcLayers L, uint64_t seed,
+                                         uint64_t step_arg, const int64_t* __restrict__ step_dev,
+                                         int off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t step = step_dev ? (uint64_t)step_dev[0] : step_arg;
+  const int s = blockIdx.y;
+  sc[(long)s * n + i] = dropconnect_scale(L.rate[s], seed, step, L.layer[s], off + i);
 }
 
 static unsigned grid_for(long n) { return std::min<unsigned>(std::max(cdiv(n, 256), 1u), 8192); }
@@ -401,6 +422,23 @@ extern "C" int pld_dropconnect_scales_dev(float* scales, int n, float rate, uint
   dropconnect_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(scales, n, rate, seed, 0,
                                                                   step_dev, layer, image_offset);
   return check_launch("dropconnect_kernel");
+}
+
+extern "C" int pld_dropconnect_scales_multi(float* scales, int n, int nl, const float* rates,
+                                            const int* layers, uint64_t seed, uint64_t step,
+                                            const int64_t* step_dev, int image_offset,
+                                            void* stream) {
+  PLD_CHECK_ARG(scales && rates && layers && n > 0 && nl > 0 && nl <= DC_MAX_LAYERS,
+                "pld_dropconnect_scales_multi: bad args");
+  DcLayers L{};
+  for (int s = 0; s < nl; ++s) {
+    PLD_CHECK_ARG(rates[s] >= 0.f && rates[s] < 1.f, "pld_dropconnect_scales_multi: bad rate");
+    L.rate[s] = rates[s];
+    L.layer[s] = layers[s];
+  }
+  dropconnect_multi_kernel<<<dim3(cdiv(n, 256), nl), 256, 0, as_stream(stream)>>>(
+      scales, n, L, seed, step, step_dev, image_offset);
+  return check_launch("dropconnect_multi_kernel");
 }
 
 extern "C" int pld_scale_per_sample(const float* x, const float* sample_scale, int n,

@@ -746,6 +746,20 @@ def dropconnect_scales(scales, rate, seed, step, layer, image_offset=0):
                                      image_offset, stream())
 
 
+def dropconnect_scales_multi(scales, rates, layers, seed, step, image_offset=0):
+    """scales [len(layers), n]: row s = dropconnect_scales(n, rates[s], ..., layers[s]) in one
+    launch; step: an int or a device int64 tensor."""
+    import ctypes
+    nl = len(layers)
+    assert scales.dim() == 2 and scales.shape[0] == nl and scales.is_contiguous()
+    r = (ctypes.c_float * nl)(*[float(x) for x in rates])
+    l = (ctypes.c_int * nl)(*[int(x) for x in layers])
+    dev = isinstance(step, torch.Tensor)
+    lib().pld_dropconnect_scales_multi(ptr(scales), scales.shape[1], nl, ctypes.cast(r, ctypes.c_void_p),
+                                       ctypes.cast(l, ctypes.c_void_p), seed, 0 if dev else step,
+                                       ptr(step) if dev else None, image_offset, stream())
+
+
 def bn_train_coeffs(mean, invstd, gamma, beta, scale, shift):
     """Training-mode BN as act-free affine coefficients (scale = gamma*invstd, shift = beta -
     mean*scale): the consuming conv's input prologue (conv_args in_scale / in_shift)."""

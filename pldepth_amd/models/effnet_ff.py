@@ -291,6 +291,13 @@ class EffNetFF:
             blk["fused_expand_dgrad"] = (self.fuse_pgemm and blk["ex"] != 1
                                          and K.pgemm_pays(cexp, blk["cin"]))
             h, w = oh, ow
+        # drop-connect keep factors of every residual block, one row each (one launch per step)
+        self._drop_layers = [li for li, blk in enumerate(self.blocks)
+                             if blk["residual"] and blk["rate"] > 0]
+        if self._drop_layers:
+            self._drop_all = torch.ones(len(self._drop_layers), B, device=dev)
+            for s, li in enumerate(self._drop_layers):
+                self.blocks[li]["drop"] = self._drop_all[s]
         new("top_pre", (B, h, w, 1280), grad=False)
         new("top_activation", (B, h, w, 1280))
         for i, (conv, bn, skip) in enumerate(self.dec):
@@ -360,6 +367,10 @@ class EffNetFF:
         else:
             self.stem_bn.apply(A["stem_pre"], rows, "swish", A["stem_activation"], training)
             x = A["stem_activation"]
+        if training and self.drop_connect and self._drop_layers:
+            K.dropconnect_scales_multi(self._drop_all,
+                                       [self.blocks[li]["rate"] for li in self._drop_layers],
+                                       self._drop_layers, self.seed, step, image_offset)
         for li, blk in enumerate(self.blocks):
             x = self._block_fwd(blk, x, training, step, li)
         h, w = x.shape[1], x.shape[2]
@@ -472,9 +483,7 @@ class EffNetFF:
             # project BN -> drop-connect -> + block input in one pass (pld_bn_scale_add_apply)
             drop = None
             if self.drop_connect and blk["rate"] > 0:
-                K.dropconnect_scales(blk["drop"], blk["rate"], self.seed, step, li,
-                                     getattr(self, "_img_off", 0))
-                drop = blk["drop"]
+                drop = blk["drop"]  # this step's keep factors (forward: one launch, all blocks)
             K.bn_scale_add_apply(A[n + "project_pre"], rows, blk["cout"], pbn.mean, pbn.invstd,
                                  pbn.gamma, pbn.beta, drop, oh * ow, x, "none", out)
             return out

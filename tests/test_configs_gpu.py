@@ -313,6 +313,21 @@ def test_dropconnect_scales_bit_exact_and_keep_rate(cuda, rate):
     assert abs(zeros / N - rate) < 5 * np.sqrt(rate * (1 - rate) / N)
 
 
+def test_dropconnect_scales_multi_layer_launch(cuda):
+    """Every block's keep factors in one launch (the forward's form): row s is layer
+    layers[s]'s stream, host step and device step alike."""
+    n, seed, rates, layers = 37, 5, [0.0125, 0.05, 0.1875, 0.5], [1, 4, 9, 15]
+    out = torch.empty(len(layers), n, device=cuda)
+    for step in (1, (1 << 33) + 3):
+        for st in (step, torch.tensor([step], dtype=torch.int64, device=cuda)):
+            out.fill_(-1.0)
+            K.dropconnect_scales_multi(out, rates, layers, seed, st, image_offset=6)
+            got = out.cpu().numpy()
+            for s, (r, li) in enumerate(zip(rates, layers)):
+                np.testing.assert_array_equal(
+                    got[s], PX.dropconnect_scales(n, r, seed, step, layer=li, image_offset=6))
+
+
 def test_sampler_draws_bit_exact_vs_philox(cuda):
     nv = np.array([1, 7, 1000, 200704], np.int32)
     d = torch.empty(4, 500, 5, dtype=torch.int32, device=cuda)
