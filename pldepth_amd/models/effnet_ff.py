@@ -291,6 +291,14 @@ class EffNetFF:
             blk["fused_expand_dgrad"] = (self.fuse_pgemm and blk["ex"] != 1
                                          and K.pgemm_pays(cexp, blk["cin"]))
             h, w = oh, ow
+        # a residual block's output gradient shares its input's gradient buffer: the block's
+        # backward reads dy (its project BN backward) before its expand dgrad accumulates onto
+        # it, which leaves dy + d(block branch) = d(block input) with no residual-add pass
+        prev = None
+        for blk in self.blocks:
+            if blk["residual"]:
+                self.gact[blk["name"] + "output"] = self.gact[prev + "output"]
+            prev = blk["name"]
         # drop-connect keep factors of every residual block, one row each (one launch per step)
         self._drop_layers = [li for li, blk in enumerate(self.blocks)
                              if blk["residual"] and blk["rate"] > 0]
@@ -650,20 +658,22 @@ class EffNetFF:
             bnp = (ebn.mean, ebn.invstd, ebn.gamma, ebn.beta)
             k12 = self._k12_buf(blk["cexp"])
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, ge, accumulate=is_tap)
+            # residual: gx_in is gy's buffer (_alloc_activations) and already holds gy
+            res = blk["residual"]
             if blk["fused_expand_dgrad"]:
                 K.bn_bwd_coeffs(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp, "swish",
                                 ebn.dgamma, ebn.dbeta, k12)
                 K.pgemm_bn_bwd(A[n + "expand_pre"], ge, B * h * w, blk["cexp"], *bnp, "swish",
-                               k12, blk["expand"].w_dg, blk["cin"], gx_in)
+                               k12, blk["expand"].w_dg, blk["cin"], gx_in, accumulate=res)
             else:
                 gpe = self._gpre_buf(A[n + "expand_pre"].shape)
                 ebn.bwd(A[n + "expand_pre"], ge, B * h * w, "swish", gpe)
                 K.conv2d_dgrad(K.conv_args(x_in, None, 1, 1, 1, 0, 0, h, w, blk["cexp"],
-                                           math=self._em(h, w)), gpe, blk["expand"].w_dg, gx_in)
+                                           math=self._em(h, w)), gpe, blk["expand"].w_dg, gx_in,
+                               acc1=res)
         else:
+            assert not blk["residual"]
             K.dwconv_dgrad(gdw, F[blk["dw"]], blk["k"], blk["s"], pt, pl, gx_in)
-        if blk["residual"]:
-            K.residual_add(gx_in, None, gy, gx_in)
 
     # ------------------------------------------------------------------ optimizer
     def adam_state(self):
