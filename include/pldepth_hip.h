@@ -205,6 +205,27 @@ int pld_filter_to_dgrad(const float* w_hwio, int kh, int kw, int cin, int cout, 
 int pld_filter_refresh(const float* w_hwio, int kh, int kw, int cin, int cout, float* w_ohwi,
                        void* w_ohwi_split, float* w_dgrad, void* w_dgrad_split, void* stream);
 
+/* The refresh of many filters in one launch (every trainable conv after the optimizer step):
+ * the caller builds a device table of descriptors once (the buffers do not move), blk0 = the
+ * running sum of the nblk of the entries before it, nblk = pld_filter_refresh_plan(...) (> 0:
+ * the filter takes the batched path; 0: refresh it with pld_filter_refresh). Same bytes as
+ * pld_filter_refresh per filter. */
+typedef struct pld_filter_refresh_desc {
+  const float* w;        /* HWIO [taps][cin][cout] */
+  float* w_nat;          /* [cout][taps][cin] */
+  void* w_nat_split;     /* or NULL */
+  float* w_dgrad;        /* [cin][taps'][cout] or NULL */
+  void* w_dgrad_split;   /* or NULL */
+  int taps, cin, cout;
+  int blk0, nblk;
+  int reserved;
+} pld_filter_refresh_desc;
+int pld_filter_refresh_plan(int kh, int kw, int cin, int cout, const void* w_hwio,
+                            const void* w_ohwi, const void* w_ohwi_split, const void* w_dgrad,
+                            const void* w_dgrad_split);
+int pld_filter_refresh_multi(const pld_filter_refresh_desc* table_dev, int count,
+                             int total_blocks, void* stream);
+
 /* per-channel column sum over `rows` rows of an [rows][c] tensor: out[c] (+)= sum_r x[r][c]
  * (bias gradient of Conv2D). ws >= pld_channel_reduce_workspace_size(rows, c). */
 size_t pld_channel_reduce_workspace_size(int64_t rows, int c);

@@ -66,6 +66,8 @@ _SIGS = {
     "pld_filter_split": (I32, [P, I64, I32, P, P]),
     "pld_filter_to_dgrad": (I32, [P, I32, I32, I32, I32, P, P]),
     "pld_filter_refresh": (I32, [P, I32, I32, I32, I32, P, P, P, P, P]),
+    "pld_filter_refresh_plan": (I32, [I32, I32, I32, I32, P, P, P, P, P]),
+    "pld_filter_refresh_multi": (I32, [P, I32, I32, P]),
     "pld_channel_reduce_workspace_size": (SZ, [I64, I32]),
     "pld_channel_sum": (I32, [P, I64, I32, P, I32, P, P]),
     "pld_bn_stats": (I32, [P, I64, I32, F32, F32, P, P, P, P, P, P]),
@@ -146,7 +148,8 @@ _NON_STATUS = {"pld_last_error", "pld_version", "pld_pgemm_ok", "pld_conv_num_ti
                "pld_sampler_workspace_size", "pld_sampler_candidates",
                "pld_sampler_compact_workspace_size", "pld_upconv_wgrad_workspace_size",
                "pld_upconv_bwd_workspace_size", "pld_se_bwd_bn_full_workspace_size",
-               "pld_dwconv_dgrad_bn_bwd_workspace_size"}
+               "pld_dwconv_dgrad_bn_bwd_workspace_size",
+               "pld_filter_refresh_plan"}
 
 
 def declared_symbols(header=HEADER):

@@ -631,12 +631,11 @@ __device__ __forceinline__ void split_chunk(const float* v, u32x4r* out) {
 // HWIO viewed as W[R = taps*cin][cout] -> native O[cout][R]: 64x64 tiles transposed through LDS
 // (row pitch 65: conflict-free both ways); every output lane writes one 8-value chunk (32 B of
 // fp32 + its 32-B split). R % 8 == 0.
-__global__ __launch_bounds__(256) void filter_native_tiled_kernel(const float* __restrict__ w,
-                                                                  int R, int cout,
-                                                                  float* __restrict__ o,
-                                                                  u32x4r* __restrict__ osplit) {
+__device__ __forceinline__ void filter_native_tile(const float* __restrict__ w, int R, int cout,
+                                                   float* __restrict__ o,
+                                                   u32x4r* __restrict__ osplit, int bx, int by) {
   __shared__ float t[64][65];
-  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int r0 = bx * 64, c0 = by * 64;
   const int tid = threadIdx.x, lc = tid & 63;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -660,16 +659,21 @@ __global__ __launch_bounds__(256) void filter_native_tiled_kernel(const float* _
   }
 }
 
+__global__ __launch_bounds__(256) void filter_native_tiled_kernel(const float* __restrict__ w,
+                                                                  int R, int cout,
+                                                                  float* __restrict__ o,
+                                                                  u32x4r* __restrict__ osplit) {
+  filter_native_tile(w, R, cout, o, osplit, blockIdx.x, blockIdx.y);
+}
+
 // HWIO -> dgrad [cin][taps'][cout] (taps flipped): a permutation of cout-long rows, one 8-value
-// chunk per thread (coalesced both sides). cout % 8 == 0.
-__global__ __launch_bounds__(256) void filter_dgrad_rows_kernel(const float* __restrict__ w,
-                                                                int taps, int cin, int cout,
-                                                                float* __restrict__ o,
-                                                                u32x4r* __restrict__ osplit) {
+// chunk per thread (coalesced both sides). cout % 8 == 0. Block b of nb.
+__device__ __forceinline__ void filter_dgrad_rows(const float* __restrict__ w, int taps, int cin,
+                                                  int cout, float* __restrict__ o,
+                                                  u32x4r* __restrict__ osplit, int b, int nb) {
   const int c8n = cout >> 3;
   const long n = (long)cin * taps * c8n;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (long)gridDim.x * blockDim.x) {
+  for (long e = (long)b * 256 + threadIdx.x; e < n; e += (long)nb * 256) {
     const int c8 = (int)(e % c8n);
     const long rest = e / c8n;
     const int tp = (int)(rest % taps), ci = (int)(rest / taps);
@@ -684,6 +688,35 @@ __global__ __launch_bounds__(256) void filter_dgrad_rows_kernel(const float* __r
       split_chunk(v, osplit + f / 4);
     }
   }
+}
+
+__global__ __launch_bounds__(256) void filter_dgrad_rows_kernel(const float* __restrict__ w,
+                                                                int taps, int cin, int cout,
+                                                                float* __restrict__ o,
+                                                                u32x4r* __restrict__ osplit) {
+  filter_dgrad_rows(w, taps, cin, cout, o, osplit, blockIdx.x, gridDim.x);
+}
+
+// Every trainable conv's refresh in one launch: a flat grid over a device table of filters, each
+// owning a contiguous block range (its native tiles, then its dgrad row blocks); a block finds
+// its filter by a wave-uniform scan of the range starts. Same bytes as pld_filter_refresh.
+static unsigned refresh_dgrad_blocks(long n8) { return std::min<unsigned>(cdiv(n8, 256), 8192); }
+
+__global__ __launch_bounds__(256) void filter_refresh_multi_kernel(
+    const pld_filter_refresh_desc* __restrict__ d, int count) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < count && d[i + 1].blk0 <= b) ++i;
+  const pld_filter_refresh_desc f = d[i];
+  const int R = f.taps * f.cin;
+  const int tx = (R + 63) / 64;
+  const int nat = tx * ((f.cout + 63) / 64);
+  const int lb = b - f.blk0;
+  if (lb < nat)
+    filter_native_tile(f.w, R, f.cout, f.w_nat, (u32x4r*)f.w_nat_split, lb % tx, lb / tx);
+  else if (f.w_dgrad)
+    filter_dgrad_rows(f.w, f.taps, f.cin, f.cout, f.w_dgrad, (u32x4r*)f.w_dgrad_split, lb - nat,
+                      f.nblk - nat);
 }
 
 // ------------------------------------------------------------------------ dispatch
@@ -1188,6 +1221,31 @@ extern "C" int pld_filter_refresh(const float* w_hwio, int kh, int kw, int cin, 
   if (!rc && w_dgrad_split)
     rc = pld_filter_split(w_dgrad, cin, taps * cout, w_dgrad_split, stream);
   return rc;
+}
+
+extern "C" int pld_filter_refresh_plan(int kh, int kw, int cin, int cout, const void* w_hwio,
+                                       const void* w_ohwi, const void* w_ohwi_split,
+                                       const void* w_dgrad, const void* w_dgrad_split) {
+  if (!w_hwio || !w_ohwi || kh <= 0 || kw <= 0 || cin <= 0 || cout <= 0) return 0;
+  if (w_dgrad_split && !w_dgrad) return 0;
+  const long R = (long)kh * kw * cin;
+  if (R % 8 || R >= (1L << 30) || !aligned16(w_ohwi) || (w_ohwi_split && !aligned16(w_ohwi_split)))
+    return 0;
+  long nblk = cdiv(R, 64) * cdiv(cout, 64);
+  if (w_dgrad) {
+    if (cout % 8 || !aligned16(w_hwio) || !aligned16(w_dgrad) ||
+        (w_dgrad_split && !aligned16(w_dgrad_split)))
+      return 0;
+    nblk += refresh_dgrad_blocks(R * cout / 8);
+  }
+  return nblk < (1L << 30) ? (int)nblk : 0;
+}
+
+extern "C" int pld_filter_refresh_multi(const pld_filter_refresh_desc* table_dev, int count,
+                                        int total_blocks, void* stream) {
+  PLD_CHECK_ARG(table_dev && count > 0 && total_blocks > 0, "pld_filter_refresh_multi: bad args");
+  filter_refresh_multi_kernel<<<total_blocks, 256, 0, as_stream(stream)>>>(table_dev, count);
+  return check_launch("filter_refresh_multi_kernel");
 }
 
 extern "C" int pld_conv2d_fwd(const pld_conv_args* a, const float* w_ohwi, const float* bias,

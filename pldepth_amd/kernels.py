@@ -442,6 +442,54 @@ def filter_refresh(w_hwio, w_nat, w_nat_split=None, w_dg=None, w_dg_split=None):
         w_dg._pld_split = w_dg_split
 
 
+class _RefreshDesc(C.Structure):
+    """Mirror of ``pld_filter_refresh_desc``."""
+    _fields_ = [("w", C.c_void_p), ("w_nat", C.c_void_p), ("w_nat_split", C.c_void_p),
+                ("w_dgrad", C.c_void_p), ("w_dgrad_split", C.c_void_p),
+                ("taps", C.c_int), ("cin", C.c_int), ("cout", C.c_int),
+                ("blk0", C.c_int), ("nblk", C.c_int), ("reserved", C.c_int)]
+
+
+class FilterRefreshBatch:
+    """Every listed filter's pld_filter_refresh in one launch (pld_filter_refresh_multi) from a
+    device descriptor table built once; filters the batched path does not take (layout or
+    alignment) keep their own pld_filter_refresh call. Entries: (w_hwio, w_nat, w_nat_split,
+    w_dg, w_dg_split), the buffers fixed for the batch's lifetime."""
+
+    def __init__(self, entries, device):
+        self.entries = list(entries)
+        descs, self.single, blk = [], [], 0
+        for e in self.entries:
+            w, wn, wns, wd, wds = e
+            kh, kw, cin, cout = w.shape
+            nb = lib().pld_filter_refresh_plan(kh, kw, cin, cout, ptr(w), ptr(wn), ptr(wns),
+                                               ptr(wd), ptr(wds))
+            if nb <= 0:
+                self.single.append(e)
+                continue
+            a = [None if t is None else ptr(t).value for t in e]
+            descs.append(_RefreshDesc(*a, kh * kw, cin, cout, blk, nb, 0))
+            blk += nb
+        self.count, self.blocks = len(descs), blk
+        self.table = None
+        if descs:
+            arr = (_RefreshDesc * len(descs))(*descs)
+            host = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy())
+            self.table = host.to(device)
+            torch.cuda.synchronize(device)
+        for w, wn, wns, wd, wds in self.entries:  # the split copies ride on their fp32 tensors
+            if wns is not None:
+                wn._pld_split = wns
+            if wds is not None:
+                wd._pld_split = wds
+
+    def __call__(self):
+        if self.count:
+            lib().pld_filter_refresh_multi(ptr(self.table), self.count, self.blocks, stream())
+        for e in self.single:
+            filter_refresh(*e)
+
+
 def filter_split(w, out=None):
     """Split a [rows][K] fp32 filter (K % 8 == 0) for the bf16x3 kernel and attach the copy to
     the fp32 tensor object (w._pld_split): conv2d_fwd / conv2d_dgrad given that same tensor use

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from .. import kernels as K
-from .engine_common import FlatStore, _BN, _Conv  # noqa: F401  (re-exported)
+from .engine_common import FlatStore, _BN, _Conv, refresh_trainable_convs  # noqa: F401  (re-exported)
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.99
@@ -242,9 +242,7 @@ class EffNetFF:
         self.norm_shift.copy_((-mean / sd).float())
 
     def refresh_trainable(self):
-        for c in self.convs:
-            if c.trainable:
-                c.refresh()
+        refresh_trainable_convs(self)
 
     # ------------------------------------------------------------------ activations
     def _alloc_activations(self):

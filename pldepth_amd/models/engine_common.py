@@ -161,3 +161,16 @@ class _Conv:
 
     def refresh(self):
         K.filter_refresh(self.w, self.w_nat, self.w_nat_x3, self.w_dg, self.w_dg_x3)
+
+
+def refresh_trainable_convs(eng):
+    """Every trainable conv's filter copies after the optimizer step, in one launch
+    (kernels.FilterRefreshBatch over a descriptor table built at the first call: the engines
+    make it eagerly, from set_weights, before any graph capture)."""
+    batch = getattr(eng, "_refresh_batch", None)
+    if batch is None:
+        assert not K._CAPTURING[0], "the refresh table must be built before graph capture"
+        batch = eng._refresh_batch = K.FilterRefreshBatch(
+            [(c.w, c.w_nat, c.w_nat_x3, c.w_dg, c.w_dg_x3) for c in eng.convs if c.trainable],
+            eng.device)
+    batch()

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from .. import kernels as K
-from .engine_common import FlatStore, _BN, _Conv
+from .engine_common import FlatStore, _BN, _Conv, refresh_trainable_convs
 
 RESNET_BN_EPS = 1.001e-5
 CAFFE_MEAN_BGR = np.array([103.939, 116.779, 123.68], np.float32)
@@ -191,9 +191,7 @@ class RedWebFF:
             c.refresh()
 
     def refresh_trainable(self):
-        for c in self.convs:
-            if c.trainable:
-                c.refresh()
+        refresh_trainable_convs(self)
 
     # ------------------------------------------------------------------ activations
     def _alloc(self):

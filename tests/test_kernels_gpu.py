@@ -1435,6 +1435,44 @@ def test_filter_refresh(cuda, kh, cin, cout):
     torch.cuda.synchronize()
 
 
+def test_filter_refresh_batch(cuda):
+    """kernels.FilterRefreshBatch (pld_filter_refresh_multi over a device table; the filters
+    the batched path does not take keep their own call) == pld_filter_refresh per filter, bit
+    for bit: the decoder shapes, a 1x1, one without a dgrad copy, unaligned ones."""
+    shapes = [(3, 1952, 672, True), (3, 912, 240, True), (3, 32, 1, True), (1, 40, 240, True),
+              (3, 12, 20, True), (3, 72, 100, True), (3, 64, 64, False), (3, 3, 32, True),
+              (1, 256, 2048, True)]
+    g = torch.Generator(device=cuda).manual_seed(7)
+    entries, refs = [], []
+    for kh, cin, cout, dgrad in shapes:
+        w = torch.randn(kh, kh, cin, cout, device=cuda, generator=g)
+        nat = torch.full((cout, kh, kh, cin), -1.0, device=cuda)
+        dg = torch.full((cin, kh, kh, cout), -1.0, device=cuda) if dgrad else None
+        ns = torch.full_like(nat, -1.0) if (kh * kh * cin) % 8 == 0 else None
+        ds = torch.full_like(dg, -1.0) if dgrad and (kh * kh * cout) % 8 == 0 else None
+        entries.append((w, nat, ns, dg, ds))
+        r = [torch.empty_like(nat), None if ns is None else torch.empty_like(ns),
+             None if dg is None else torch.empty_like(dg), None if ds is None else torch.empty_like(ds)]
+        K.filter_refresh(w, *r)
+        refs.append(r)
+    batch = K.FilterRefreshBatch(entries, cuda)
+    assert batch.count == 5 and len(batch.single) == 4  # both paths exercised
+    batch()
+    torch.cuda.synchronize()
+    for (w, *got), ref in zip(entries, refs):
+        for a, b in zip(got, ref):
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert torch.equal(a, b), w.shape
+    # a second call (the per-step form) rewrites the same bytes
+    for _, nat, *_ in entries:
+        nat.fill_(0.0)
+    batch()
+    torch.cuda.synchronize()
+    for (w, nat, *_), ref in zip(entries, refs):
+        assert torch.equal(nat, ref[0])
+
+
 @pytest.mark.parametrize("n,h,w,pt,pl", [(2, 64, 64, 0, 0), (1, 37, 51, 1, 1), (3, 18, 70, 0, 1),
                                           (1, 448, 448, 0, 0)])
 def test_stem3x3(cuda, n, h, w, pt, pl):
