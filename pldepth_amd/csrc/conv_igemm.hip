@@ -579,6 +579,33 @@ __global__ __launch_bounds__(256) void stride_scatter4_kernel(const float* __res
   }
 }
 
+// the accumulate form (every destination += t): only the stride grid's pixels change, so the
+// walk is over t's [n][oh][ow][C / 4] quads (read t, read-modify-write one destination quad):
+// a quarter of the input-resolution traffic of the full-grid form at stride 2
+__global__ __launch_bounds__(256) void stride_scatter4_acc_kernel(const float* __restrict__ t,
+                                                                  int total4, FastDiv dC4,
+                                                                  FastDiv dOW, FastDiv dOH, int h,
+                                                                  int w, int sh, int sw, int C,
+                                                                  float* out1, int c1,
+                                                                  float* out2) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    const uint32_t opix = dC4.div((uint32_t)i);
+    const int c = 4 * (i - (int)opix * (int)dC4.d);
+    const uint32_t r = dOW.div(opix);
+    const int xs = (int)(opix - r * dOW.d);
+    const uint32_t img = dOH.div(r);
+    const int ys = (int)(r - img * dOH.d);
+    const int y = ys * sh, x = xs * sw;
+    if (y >= h || x >= w) continue;
+    const long pix = ((long)img * h + y) * w + x;
+    const float4 v = *reinterpret_cast<const float4*>(t + (long)opix * C + c);
+    float4* d = c < c1 ? reinterpret_cast<float4*>(out1 + pix * c1 + c)
+                       : reinterpret_cast<float4*>(out2 + pix * (C - c1) + (c - c1));
+    const float4 o = *d;
+    *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+  }
+}
+
 // HWIO [kh][kw][ci][co] -> [co][kh][kw][ci]
 __global__ void filter_native_kernel(const float* __restrict__ w, int taps, int cin, int cout,
                                      float* __restrict__ o) {
@@ -1552,6 +1579,13 @@ extern "C" int pld_conv2d_dgrad(const pld_conv_args* a, const float* dy, const f
     const long total = (long)a->n * a->h * a->w * C;
     if (C % 4 == 0 && a->c1 % 4 == 0 && aligned16(t) && aligned16(dx1) &&
         (!dx2 || aligned16(dx2))) {
+      if (accumulate1 && (!dx2 || accumulate2)) {
+        const long tq = (long)a->n * a->oh * a->ow * (C / 4);
+        stride_scatter4_acc_kernel<<<std::min<unsigned>(cdiv(tq, 256), 16384), 256, 0, st>>>(
+            t, (int)tq, FastDiv((uint32_t)(C / 4)), FastDiv((uint32_t)a->ow),
+            FastDiv((uint32_t)a->oh), a->h, a->w, a->sh, a->sw, C, dx1, a->c1, dx2);
+        return check_launch("stride_scatter4_acc_kernel");
+      }
       const int total4 = (int)(total / 4);
       stride_scatter4_kernel<<<std::min<unsigned>(cdiv(total4, 256), 16384), 256, 0, st>>>(
           t, total4, FastDiv((uint32_t)(C / 4)), FastDiv((uint32_t)a->w),
