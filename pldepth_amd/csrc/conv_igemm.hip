@@ -486,6 +486,33 @@ __global__ __launch_bounds__(256) void splitk_group_kernel(const float* __restri
   part[(long)blockIdx.y * n + i] = s;
 }
 
+// both levels of that reduction in one launch, in the same order (group g sums its SPLIT_GROUP
+// slabs in order; the groups are then summed in order): a 256-thread block is EL elements x G
+// group lanes (G = the group count rounded up to a power of two <= 32), the group sums meet in
+// LDS. Bit-identical to splitk_group_kernel + splitk_reduce_kernel, one dependent launch less.
+template <int G>
+__global__ __launch_bounds__(256) void splitk_reduce2_kernel(const float* __restrict__ ws,
+                                                             int splits, long n,
+                                                             float* __restrict__ dw, int acc) {
+  constexpr int EL = 256 / G;
+  __shared__ float red[G][EL];
+  const int e = threadIdx.x % EL, g = threadIdx.x / EL;
+  const long i = (long)blockIdx.x * EL + e;
+  const int groups = (splits + SPLIT_GROUP - 1) / SPLIT_GROUP;
+  float s = 0.f;
+  if (i < n && g < groups) {
+    const int z1 = min(splits, (g + 1) * SPLIT_GROUP);
+    for (int z = g * SPLIT_GROUP; z < z1; ++z) s += ws[(long)z * n + i];
+  }
+  red[g][e] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = 0.f;
+    for (int k = 0; k < groups; ++k) t += red[k][e];
+    dw[i] = acc ? dw[i] + t : t;
+  }
+}
+
 // ordered split-K reduction of forward / dgrad slabs with bias and two-destination routing
 __global__ __launch_bounds__(256) void splitk_out_kernel(const float* __restrict__ ws, int splits,
                                                          long M, int N, const float* bias,
@@ -1827,6 +1854,16 @@ extern "C" int pld_conv2d_wgrad(const pld_conv_args* a, const float* dy, float* 
   const long n = (long)M * N;
   const float* src = (const float*)ws;
   int terms = splits;
+  if (splits > 2 * SPLIT_GROUP && splits <= 32 * SPLIT_GROUP) {
+    const int groups = (splits + SPLIT_GROUP - 1) / SPLIT_GROUP;
+    const int G = groups <= 4 ? 4 : groups <= 8 ? 8 : groups <= 16 ? 16 : 32;
+    const unsigned blocks = (unsigned)cdiv(n, 256 / G);
+    if (G == 4) splitk_reduce2_kernel<4><<<blocks, 256, 0, st>>>(src, splits, n, dw, accumulate);
+    else if (G == 8) splitk_reduce2_kernel<8><<<blocks, 256, 0, st>>>(src, splits, n, dw, accumulate);
+    else if (G == 16) splitk_reduce2_kernel<16><<<blocks, 256, 0, st>>>(src, splits, n, dw, accumulate);
+    else splitk_reduce2_kernel<32><<<blocks, 256, 0, st>>>(src, splits, n, dw, accumulate);
+    return check_launch("splitk_reduce2_kernel");
+  }
   if (splits > 2 * SPLIT_GROUP) {
     const int groups = (splits + SPLIT_GROUP - 1) / SPLIT_GROUP;
     float* part = (float*)ws + (long)splits * n;
