@@ -3,6 +3,8 @@ import ctypes as C
 import os
 import subprocess
 
+import pytest
+
 from pldepth_amd import _lib
 
 
@@ -50,6 +52,25 @@ def test_host_only_entry_points():
     assert lib.pld_conv2d_fwd_workspace_size(C.byref(a)) == 0
     a.tile = nt // 2
     assert lib.pld_conv2d_fwd_workspace_size(C.byref(a)) >= 2 * 49 * 64 * 4
+
+
+def test_filter_refresh_plan_and_descriptor_layout():
+    """pld_filter_refresh_plan (host arithmetic only): the block count of a filter's batched
+    refresh, 0 where the batched path does not apply; the ctypes descriptor matches the
+    header's pld_filter_refresh_desc (5 pointers + 6 ints = 64 B)."""
+    from pldepth_amd import kernels as K
+    lib = _lib.lib()
+    p, q = C.c_void_p(1 << 20), C.c_void_p((1 << 20) + 4)  # 16-byte aligned / not
+    # 3x3, 64 -> 64: 9 x 1 native tiles + ceil(576 * 64 / 8 / 256) = 18 dgrad blocks
+    assert lib.pld_filter_refresh_plan(3, 3, 64, 64, p, p, p, p, p) == 9 + 18
+    assert lib.pld_filter_refresh_plan(3, 3, 64, 64, p, p, None, None, None) == 9
+    assert lib.pld_filter_refresh_plan(3, 3, 3, 32, p, p, p, p, p) == 0   # R = 27 % 8
+    assert lib.pld_filter_refresh_plan(3, 3, 64, 100, p, p, p, p, p) == 0  # dgrad cout % 8
+    assert lib.pld_filter_refresh_plan(3, 3, 64, 64, p, q, p, p, p) == 0   # misaligned
+    assert lib.pld_filter_refresh_plan(3, 3, 64, 64, p, p, p, None, p) == 0  # split w/o dgrad
+    assert C.sizeof(K._RefreshDesc) == 64
+    with pytest.raises(_lib.PLDError):
+        lib.pld_filter_refresh_multi(None, 1, 1, None)
 
 
 def test_header_documents_reference_replacements():
