@@ -141,10 +141,13 @@ int pld_conv_num_schedules(int math);
  * other shapes run the default tile), an fp32 tile, an fp32 tile with split-K, a bf16x3 tile
  * stream (a 1-D grid of persistent workgroups walking (tile, K-step) ranges: whole tiles when
  * they fill the GPU, else an even cut of the K steps with a fixup pass over the cut tiles; no
- * input prologue: such calls run the default tile); -1 if out of range. WGRAD sizes its own
- * split: only the tile classes are distinct for it. */
+ * input prologue: such calls run the default tile), a bf16x3 row-band halo kernel (3x3 stride-1
+ * 'same' convs on maps up to 56 pixels wide, forward view: each 32-channel chunk of the input
+ * band staged once for its 9 taps; "x3halo/BMxBN", with split-K over whole chunks
+ * "x3halosplit/BMxBN"; other shapes run the default tile); -1 if out of range. WGRAD sizes its
+ * own split: only the tile classes are distinct for it. */
 enum { PLD_SCHED_X3 = 0, PLD_SCHED_X3_SPLIT = 1, PLD_SCHED_X3_PATCH = 2, PLD_SCHED_FP32 = 3,
-       PLD_SCHED_FP32_SPLIT = 4, PLD_SCHED_X3_STREAM = 5 };
+       PLD_SCHED_FP32_SPLIT = 4, PLD_SCHED_X3_STREAM = 5, PLD_SCHED_X3_HALO = 6 };
 int pld_conv_schedule_class(int math, int idx);
 /* a stable text name of schedule `idx` ("x3/128x128", "x3split/256x64", "x3patch/32",
  * "fp32/128x96", "fp32split/256x32"; NULL if out of range): a persisted tuning table keys its

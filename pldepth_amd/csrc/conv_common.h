@@ -50,6 +50,10 @@ struct GemmConvParams {
   // pld's stream fixup kernel sums in K order and stores through the epilogue.
   int sk_nk, sk_tiles, sk_nnb, sk_align;
   float* sk_slab;
+  int sk_q;  // steps per cut unit of a non-aligned range (0 / 1: any step)
+  // row-band halo kernel (conv_x3_halo.hip): workgroup order, 0 = N tiles fastest, 1 = M tiles
+  // fastest (the workgroups an XCD runs together share one filter panel)
+  int raster;
 };
 
 // first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)
@@ -61,12 +65,16 @@ __device__ __forceinline__ int xcd_order(int flat, int nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
 }
 
+// (sk_q > 1: non-aligned ranges cut on multiples of sk_q steps — the halo kernel's chunks)
 __host__ __device__ inline long sk_begin(const GemmConvParams& p, long w, long G) {
-  return p.sk_align ? (w * p.sk_tiles / G) * p.sk_nk : w * ((long)p.sk_tiles * p.sk_nk) / G;
+  if (p.sk_align) return (w * p.sk_tiles / G) * p.sk_nk;
+  const long q = p.sk_q > 1 ? p.sk_q : 1;
+  return (w * ((long)p.sk_tiles * p.sk_nk / q) / G) * q;
 }
 // the workgroup whose range holds global step s (non-aligned schedule)
 __host__ __device__ inline long sk_owner(const GemmConvParams& p, long s, long G) {
-  return ((s + 1) * G - 1) / ((long)p.sk_tiles * p.sk_nk);
+  const long q = p.sk_q > 1 ? p.sk_q : 1;
+  return ((s / q + 1) * G - 1) / ((long)p.sk_tiles * p.sk_nk / q);
 }
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));

@@ -926,6 +926,13 @@ extern "C" int pld__x3_patch_wgrad_ok(const GemmConvParams* p);
 extern "C" int pld__x3_patch_wgrad_launch(GemmConvParams* p, int splits, void* stream);
 extern "C" int pld__x3_patch_wgrad_cw(int N);
 extern "C" int pld__x3_patch_wgrad_th(int N);
+extern "C" int pld__x3_num_halo(void);
+extern "C" int pld__x3_halo_dims(int cfg, int* bm, int* bn, int* tm, int* tn);
+extern "C" int pld__x3_halo_ok(const GemmConvParams* p);
+extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int sk_grid,
+                                   void* stream);
+extern "C" int pld__x3_halo_stream_plan(GemmConvParams* p, int cfg);
+extern "C" size_t pld__x3_halo_stream_slab_bytes(int cfg, int G, int aligned);
 constexpr int X3_BK = 32;
 // bytes of a pre-split [N][K] filter (same size as fp32), 256-byte aligned
 static size_t x3_split_bytes(long N, long K) { return ((size_t)N * K * 4 + 255) / 256 * 256; }
@@ -938,18 +945,22 @@ static bool x3_fwd_geom(int C, int c1, bool prologue, int taps) {
 // Schedule index space under PLD_MATH_BF16X3: [0, 2 n3) bf16x3 tiles (x split-K), [2 n3,
 // 2 n3 + np) the bf16x3 patch kernel (3x3, 32-channel inputs; other shapes take the default
 // tile), [2 n3 + np, 3 n3 + np) the bf16x3 tiles as a tile stream (conv_x3_kernel STREAM: a
-// 1-D grid walking (tile, K-step) ranges), then the exact-fp32 schedules — the per-shape
-// autotuner may keep fp32 where it is faster (e.g. HBM-bound K <= 32 convs); it is never less
-// accurate. Resolves (math, eligible geometry, tile) to (x3 kernel?, patch kernel?, stream?,
-// tile in that space).
-static int x3_sched_count() { return 3 * pld__x3_num_cfg() + pld__x3_num_patch(); }
+// 1-D grid walking (tile, K-step) ranges), [3 n3 + np, 3 n3 + np + 3 nh) the row-band halo
+// kernel (conv_x3_halo.hip: grid, split-K over whole chunks, tile stream), then the exact-fp32
+// schedules — the
+// per-shape autotuner may keep fp32 where it is faster (e.g. HBM-bound K <= 32 convs); it is
+// never less accurate. Resolves (math, eligible geometry, tile) to (x3 kernel?, patch kernel?,
+// stream?, halo?, tile in that space; halo: [0, 3 nh)).
+static int x3_halo_base() { return 3 * pld__x3_num_cfg() + pld__x3_num_patch(); }
+static int x3_sched_count() { return x3_halo_base() + 3 * pld__x3_num_halo(); }
 static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t,
-                          bool* patch = nullptr, bool* stream = nullptr) {
+                          bool* patch = nullptr, bool* stream = nullptr, bool* halo = nullptr) {
   const int n3 = pld__x3_num_cfg(), np = pld__x3_num_patch(), nx = x3_sched_count();
   x3 = false;
   t = tile;
   if (patch) *patch = false;
   if (stream) *stream = false;
+  if (halo) *halo = false;
   if (math != PLD_MATH_BF16X3) return;
   if (tile >= nx) {
     t = tile - nx;
@@ -960,7 +971,10 @@ static void resolve_sched(int math, bool geom_ok, int tile, bool& x3, int& t,
     return;
   }
   x3 = true;
-  if (tile >= 2 * n3 + np) {  // tile stream of cfg tile - (2 n3 + np); callers that cannot
+  if (tile >= x3_halo_base()) {  // halo schedule tile - base (callers that cannot: default)
+    t = halo ? tile - x3_halo_base() : -1;
+    if (halo) *halo = true;
+  } else if (tile >= 2 * n3 + np) {  // tile stream of cfg tile - (2 n3 + np); callers that cannot
     t = stream ? tile - 2 * n3 - np : -1;  // run it take the default tile
     if (stream) *stream = true;
   } else if (tile >= 2 * n3) {
@@ -1027,6 +1041,28 @@ static void x3_fwd_plan(long M, long N, long K, long ktiles, int tile, int& cfg,
   kt_per = (int)((ktiles + s - 1) / s);
   splits = (int)((ktiles + kt_per - 1) / kt_per);
 }
+
+// halo plan (h in [0, 3 nh): cfg h % nh; nh <= h < 2 nh: split-K over whole chunks, enough
+// workgroups for two rounds of the 256 CUs (one resident each), >= 4 chunks per split; h >= 2 nh:
+// the tile stream, planned by pld__x3_halo_stream_plan (splits = 1 here)
+static void x3_halo_plan(long M, long N, int kc_tap, int h, int& cfg, int& splits,
+                         int& kt_per) {
+  const int nh = pld__x3_num_halo();
+  cfg = h % nh;
+  int bm, bn, tm, tn;
+  pld__x3_halo_dims(cfg, &bm, &bn, &tm, &tn);
+  const long blocks = (long)cdiv(M, bm) * cdiv(N, bn);
+  long s = 1;
+  if (h >= nh && h < 2 * nh) {
+    s = std::max<long>(1, (512 + blocks - 1) / blocks);
+    s = std::min<long>(s, std::max<long>(1, kc_tap / 4));
+    s = std::min<long>(s, 16);
+  }
+  const long per = (kc_tap + s - 1) / s;  // chunks per split
+  kt_per = (int)(per * 9);
+  splits = (int)((kc_tap + per - 1) / per);
+}
+static bool x3_halo_is_stream(int h) { return h >= 2 * pld__x3_num_halo(); }
 
 // tile-stream plan: T tiles of nk K-steps on occ resident workgroups per CU. As many tiles as
 // resident slots or more: whole tiles per workgroup, balanced (the pipeline runs on from tile to
@@ -1104,9 +1140,13 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
                         size_t ws_bytes, hipStream_t st, const char* who, int math = 0) {
   int cfg, splits, kt_per;
   bool x3;
-  bool patch, stream;
+  bool patch, stream, halo;
   resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
-                tile, &patch, &stream);
+                tile, &patch, &stream, &halo);
+  if (halo && !pld__x3_halo_ok(&p)) {  // halo schedule on another shape: default tile
+    halo = false;
+    tile = -1;
+  }
   const long in_bytes = (long)p.n * p.h * p.w * std::max(p.c1, p.c2) * 4;
   if (stream && (p.in_scale || in_bytes >= MAX_RECORDS)) {  // stream: no prologue, whole-tensor
     stream = false;                                         // descriptors
@@ -1132,6 +1172,41 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
       p.bsplit = wsp;
     }
     if (patch) return pld__x3_patch_launch(&p, tile, st);
+    if (halo) {
+      p.kc1 = (int)cdiv(p.c1, X3_BK);
+      p.kc_tap = p.kc1 + (int)cdiv(p.c2, X3_BK);
+      x3_halo_plan(p.M, p.N, p.kc_tap, tile, cfg, splits, kt_per);
+      if (splits == 1) {
+        p.ktiles_per_split = 0;
+        p.zstride = 0;
+        int bm, bn, tm, tn;
+        pld__x3_halo_dims(cfg, &bm, &bn, &tm, &tn);
+        int G = 0;
+        if (x3_halo_is_stream(tile)) {
+          G = pld__x3_halo_stream_plan(&p, cfg);
+          const size_t need = pld__x3_halo_stream_slab_bytes(cfg, G, p.sk_align);
+          PLD_CHECK_ARG(need == 0 || (ws && ws_bytes >= need),
+                        "%s: halo tile-stream workspace %zu < %zu bytes", who, ws_bytes, need);
+          p.sk_slab = need ? (float*)ws : nullptr;
+        }
+        fwd_stats_attach(p, bm, tm);
+        return pld__x3_halo_launch(&p, cfg, 1, G, st);
+      }
+      const size_t need = sizeof(float) * (size_t)splits * p.M * p.N;
+      PLD_CHECK_ARG(ws && ws_bytes >= need, "%s: split-K workspace %zu < %zu bytes", who,
+                    ws_bytes, need);
+      GemmConvParams q = p;
+      q.ktiles_per_split = kt_per;
+      q.zstride = (long)p.M * p.N;
+      q.out1 = (float*)ws;
+      int rc = pld__x3_halo_launch(&q, cfg, splits, 0, st);
+      if (rc) return rc;
+      const long n = (long)p.M * p.N;
+      splitk_out_kernel<<<std::min<unsigned>(cdiv(n, 256), 8192), 256, 0, st>>>(
+          (const float*)ws, splits, p.M, p.N, p.bias, p.out1, p.ld1, p.acc1, p.out2, p.ld2,
+          p.acc2, p.split);
+      return check_launch("splitk_out_kernel");
+    }
     p.kc_tap = x3_kc_tap(p.kh * p.kw, p.c1, p.c2);
     p.kc1 = (int)cdiv(p.c1, X3_BK);
     if (stream) {
@@ -1203,10 +1278,22 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
 static size_t fwd_ws_bytes(long M, long N, long K, int taps, int c1, int c2, int tile,
                            int math = 0, bool geom = false, bool have_split = true) {
   int cfg, splits, kt_per;
-  bool x3, stream;
-  resolve_sched(math, geom, tile, x3, tile, nullptr, &stream);
+  bool x3, stream, halo;
+  resolve_sched(math, geom, tile, x3, tile, nullptr, &stream, &halo);
   size_t b;
-  if (stream) {  // (an input prologue runs on the default tile: no workspace either way)
+  if (halo) {  // (a shape the halo kernel does not take runs the default tile: no workspace)
+    const int kc = (int)(cdiv(c1, X3_BK) + cdiv(c2, X3_BK));
+    x3_halo_plan(M, N, kc, tile, cfg, splits, kt_per);
+    b = splits > 1 ? sizeof(float) * (size_t)splits * M * N : 0;
+    if (x3_halo_is_stream(tile)) {
+      GemmConvParams q{};
+      q.M = (int)M;
+      q.N = (int)N;
+      q.kc_tap = kc;
+      const int G = pld__x3_halo_stream_plan(&q, cfg);
+      b = pld__x3_halo_stream_slab_bytes(cfg, G, q.sk_align);
+    }
+  } else if (stream) {  // (an input prologue runs on the default tile: no workspace either way)
     GemmConvParams q{};
     q.M = (int)M;
     q.N = (int)N;
@@ -1428,7 +1515,8 @@ extern "C" int pld_conv_schedule_class(int math, int idx) {
   if (idx < n3) return PLD_SCHED_X3;
   if (idx < 2 * n3) return PLD_SCHED_X3_SPLIT;
   if (idx < 2 * n3 + np) return PLD_SCHED_X3_PATCH;
-  if (idx < nx) return PLD_SCHED_X3_STREAM;
+  if (idx < x3_halo_base()) return PLD_SCHED_X3_STREAM;
+  if (idx < nx) return PLD_SCHED_X3_HALO;
   return idx - nx < nf ? PLD_SCHED_FP32 : PLD_SCHED_FP32_SPLIT;
 }
 
@@ -1455,6 +1543,13 @@ extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
     case PLD_SCHED_X3_PATCH:
       snprintf(out, 24, "x3patch/%d", pld__x3_patch_bn(idx - 2 * n3));
       break;
+    case PLD_SCHED_X3_HALO: {
+      const int h = idx - x3_halo_base(), nh = pld__x3_num_halo();
+      pld__x3_halo_dims(h % nh, &bm, &bn, &tm, &tn);
+      snprintf(out, 24, "%s/%dx%d", h < nh ? "x3halo" : h < 2 * nh ? "x3halosplit" : "x3halostream",
+               bm, bn);
+      break;
+    }
     default: {
       const TileCfg& t = kTiles[(idx - nx) % kNumCfg];
       snprintf(out, 24, "%s/%dx%d", cls == PLD_SCHED_FP32 ? "fp32" : "fp32split", t.bm, t.bn);
@@ -1505,6 +1600,16 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
     return "thin1x1_kernel";
   }
   if (kind == PLD_KIND_FP32) return "conv_igemm_kernel";
+  if (mode != 2 && pld_conv_schedule_class(a->math, a->tile) == PLD_SCHED_X3_HALO) {
+    // FWD view (dgrad: the input is dY, cout channels, one source): pld__x3_halo_ok's geometry
+    const int c1 = mode == 0 ? a->c1 : a->cout, c2 = mode == 0 ? a->c2 : 0;
+    const int w = mode == 0 ? a->w : a->ow, h = mode == 0 ? a->h : a->oh;
+    const int ow = mode == 0 ? a->ow : a->w, oh = mode == 0 ? a->oh : a->h;
+    const bool ok = a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 && a->in_scale == nullptr &&
+                    oh == h && ow == w && w <= 56 && c1 % 8 == 0 && c2 % 8 == 0 &&
+                    a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 && a->pad_l <= 2;
+    return ok ? "conv_x3_halo_kernel" : "conv_x3_kernel";
+  }
   if (pld_conv_schedule_class(a->math, a->tile) != PLD_SCHED_X3_PATCH) return "conv_x3_kernel";
   const int cfg = a->tile - 2 * pld__x3_num_cfg();
   if (mode == 2)

@@ -360,6 +360,15 @@ def _patch_ok(mode, a):
     return (a.c1 % 16 == 0 and a.c2 % 16 == 0) if mode == "fwd" else a.cout % 16 == 0
 
 
+def _halo_ok(mode, a):
+    """Shapes the bf16x3 row-band halo kernel takes (pld__x3_halo_ok, FWD view of fwd / dgrad):
+    3x3 stride 1 'same', maps up to 56 pixels wide, channels in 8s."""
+    if (a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1 or a.in_scale or mode == "wgrad"
+            or a.oh != a.h or a.ow != a.w or a.w > 56):
+        return False
+    return (a.c1 % 8 == 0 and a.c2 % 8 == 0) if mode == "fwd" else a.cout % 8 == 0
+
+
 def _schedules(mode, math, a=None):
     """Schedule indices worth timing (pld_conv_args.tile): fwd/dgrad every tile x split-K
     schedule (+ the patch kernel where it applies, + the tile streams); wgrad sizes its own
@@ -378,6 +387,8 @@ def _schedules(mode, math, a=None):
         if c == 5 and a is not None and a.in_scale:
             continue
         if c == 2 and (a is None or not _patch_ok(mode, a)):
+            continue
+        if c == 6 and (a is None or not _halo_ok(mode, a)):
             continue
         out.append(i)
     return out

@@ -262,7 +262,7 @@ class RedWebFF:
 
     # ------------------------------------------------------------------ forward
     def _math(self, conv, oh=None, ow=None, bwd=False):
-        if self.enc_math == "auto":
+        if self.enc_math in ("auto", "fp32"):  # 'auto' and 'mixed'
             exact = self.exact_bwd if bwd else self.exact_stages + tuple(self.exact_fwd_extra)
             if exact and conv.name.startswith(tuple(exact)):
                 return "fp32"

@@ -271,6 +271,57 @@ def test_conv_every_schedule(cuda, case, math):
 
 
 @pytest.mark.parametrize("case", [
+    # dec0-like: 14-wide map, 12 chunks (split-K into 3 x 4 chunks), bias, N tail
+    (2, 14, 14, 320, 64, 200, True),
+    # dec1-like: 28 x 28 concat of two ragged (16-channel tail) sources, N = 240
+    (2, 28, 28, 80, 48, 240, False),
+    # dec2-like: the widest map the kernel takes (56), patch rows = BM + 114
+    (1, 56, 56, 96, 0, 144, True),
+    # a band straddling images on a map narrower than a tile row, odd width and height
+    (3, 9, 13, 40, 24, 72, True)])
+def test_conv_halo_schedules(cuda, case):
+    """The row-band halo kernel (every x3halo / x3halosplit schedule): fwd with bias and
+    accumulate, dgrad into a concat's two destinations (one accumulating), against fp64; the
+    kernel names the call reports (pld_conv_kernel_name) are the halo kernel's."""
+    n, h, w, c1, c2, cout, has_bias = case
+    torch.manual_seed(11)
+    x1 = torch.randn(n, h, w, c1, dtype=torch.float64)
+    x2 = torch.randn(n, h, w, c2, dtype=torch.float64) if c2 else None
+    wt = torch.randn(3, 3, c1 + c2, cout, dtype=torch.float64) / np.sqrt(9 * (c1 + c2))
+    b = torch.randn(cout, dtype=torch.float64) if has_bias else None
+    x1r = x1.clone().requires_grad_(True)
+    x2r = x2.clone().requires_grad_(True) if x2 is not None else None
+    y_ref = _ref_conv(x1r, x2r, wt, b, 3, 1, 1, 1, 1, 1)
+    dy = torch.randn_like(y_ref)
+    y_ref.backward(dy)
+    gx1, gx2 = dev(x1, cuda), (dev(x2, cuda) if c2 else None)
+    gw = dev(wt, cuda)
+    wn, wd = K.filter_to_native(gw), K.filter_to_dgrad(gw)
+    K.filter_split(wn, torch.empty_like(wn))
+    gb, gdy = (dev(b, cuda) if has_bias else None), dev(dy, cuda)
+    m = K.MATH["bf16x3"]
+    halo = [t for t in range(_lib.lib().pld_conv_num_schedules(m))
+            if _lib.lib().pld_conv_schedule_class(m, t) == 6]
+    assert len(halo) >= 2 and all(K.schedule_desc(m, t).startswith("x3halo") for t in halo)
+    for t in halo:
+        args = K.conv_args(gx1, gx2, 3, 3, 1, 1, 1, h, w, cout, math="bf16x3")
+        args.tile = t
+        for mode in (0, 1):
+            assert _lib.lib().pld_conv_kernel_name(C.byref(args), mode) == b"conv_x3_halo_kernel"
+        y = torch.full((n, h, w, cout), 0.5, device=cuda)
+        K.conv2d_fwd(args, wn, gb, y, accumulate=True)
+        dx1 = torch.empty_like(gx1)
+        dx2 = torch.full_like(gx2, 1.0) if c2 else None
+        K.conv2d_dgrad(args, gdy, wd, dx1, dx2, acc2=True)
+        torch.cuda.synchronize()
+        name = K.schedule_desc(m, t)
+        assert rel_err(y - 0.5, y_ref) < CONV_TOL["bf16x3"], (name, rel_err(y - 0.5, y_ref))
+        assert rel_err(dx1, x1r.grad) < CONV_TOL["bf16x3"], name
+        if c2:
+            assert rel_err(dx2 - 1.0, x2r.grad) < CONV_TOL["bf16x3"], name
+
+
+@pytest.mark.parametrize("case", [
     # 1x1 on a 2 x 128 x 128 map: enough tiles to give workgroups several whole tiles (aligned
     # ranges: the pipeline runs on across tile boundaries); its wgrad (K = 32768 pixels) cuts
     # each tile over dozens of workgroups (fixup sums)

@@ -44,6 +44,23 @@ VARIANTS = {
     "fp32_all": (("",), ("",)),
     "fp32_all_dref": (("",), ("",)),
 }
+# the batch-2 'mixed' case of tests/test_configs_gpu.py::test_cfg3_redweb_448 (PLD_EXP_CASE=b2):
+# which FFL2 conv carries the error on ffl2/block_down/bn3/gamma
+FFL2_DOWN = "ffl2/block_down"
+VARIANTS_B2 = {
+    "mixed": ((), ()),
+    "ffl2_down_fwd": ((FFL2_DOWN,), ()),
+    "ffl2_down_bwd": ((), (FFL2_DOWN,)),
+    "ffl2_down_fwdbwd": ((FFL2_DOWN,), (FFL2_DOWN,)),
+    "ffl2_fwdbwd": (("ffl2",), ("ffl2",)),
+    "ffl_fwdbwd": (("ffl",), ("ffl",)),
+    "dec_all_fwdbwd": (("ffl", "aol"), ("ffl", "aol")),
+}
+for _i in range(6):
+    _n = f"{FFL2_DOWN}/conv{_i}"
+    VARIANTS_B2[f"ffl2_down_conv{_i}_fwdbwd"] = ((_n,), (_n,))
+for _n in ("ffl2/conv0", "ffl2/conv1", "ffl2/block_left"):
+    VARIANTS_B2[_n.replace("/", "_") + "_fwdbwd"] = ((_n,), (_n,))
 
 
 def rel(a, b):
@@ -63,20 +80,37 @@ def _heartbeat():
     threading.Thread(target=beat, daemon=True).start()
 
 
-def main():
-    names = sys.argv[1:] or list(VARIANTS)
-    _heartbeat()
-    torch.cuda.set_device(0)
-    K.set_conv_math("auto")
-    n_tab, sha = K.use_schedule_table()
-    B, H, R, L = 32, 448, 100, 5
-    rng = np.random.default_rng(32)
-    x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
+def _rankings(rng, B, H, R, L):
     idx = rng.integers(0, H * H, (B, R, L))
     lab = rng.permutation(B * R * L).reshape(B, R, L) / (B * R * L)
     lab = -np.sort(-lab, axis=-1)
-    y = np.ascontiguousarray(np.stack([idx.astype(np.float32), lab.astype(np.float32)], -1))
-    eng = RedWebFF((H, H, 3), B, seed=0, conv_math="auto")
+    return np.ascontiguousarray(np.stack([idx.astype(np.float32), lab.astype(np.float32)], -1))
+
+
+def main():
+    case = os.environ.get("PLD_EXP_CASE", "b32")
+    table = VARIANTS if case == "b32" else VARIANTS_B2
+    names = sys.argv[1:] or list(table)
+    _heartbeat()
+    torch.cuda.set_device(0)
+    H, R, L = 448, 100, 5
+    if case == "b32":
+        math = "auto"
+        K.set_conv_math(math)
+        n_tab, sha = K.use_schedule_table()
+        B = 32
+        rng = np.random.default_rng(32)
+        x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
+        y = _rankings(rng, B, H, R, L)
+    else:
+        # exactly test_cfg3_redweb_448: built-in schedules (fixed_schedules), seed 4
+        math, sha, B = "mixed", "builtin", 2
+        K.AUTOTUNE = False
+        K._TILE_CACHE.clear()
+        rng = np.random.default_rng(4)
+        x = preprocess_input(rng.random((B, H, H, 3)).astype(np.float32))
+        y = _rankings(rng, B, H, R, L)
+    eng = RedWebFF((H, H, 3), B, seed=0, conv_math=math)
     W = eng.get_weights()
     P = {k: torch.tensor(v, dtype=torch.float64) for k, v in W.items()}
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in W.items()}
@@ -123,7 +157,7 @@ def main():
            "fp32_restatement_native_conv": e32b, "variants": {}}
     yt = torch.from_numpy(y).cuda()
     for v in names:
-        fwd, bwd = VARIANTS[v]
+        fwd, bwd = table[v]
         eng.exact_fwd_extra, eng.exact_bwd = fwd, bwd
         eng.set_weights(W)
         eng.act["input"].copy_(torch.from_numpy(x))
@@ -149,6 +183,13 @@ def main():
         eh = {k: rel(hip[k], g64h[k]) for k in e32}
         del g64h
         strict_fail = {k: (eh[k], e32[k]) for k in e32 if e32[k] <= TOL and eh[k] > TOL}
+        if e32b:
+            # the round-6 bar: against the worse of the two fp32 restatements
+            worse = {k: max(e32[k], e32b[k]) for k in e32}
+            ratio = sorted(((eh[k] / max(worse[k], 1e-30), k, eh[k], e32[k], e32b[k])
+                            for k in e32 if eh[k] > TOL), reverse=True)[:8]
+            print(f"  {v}: HIP/worse-fp32 over 1e-3: " + ", ".join(
+                f"{k} {r:.2f} ({a:.2e} vs {b:.2e}/{c:.2e})" for r, k, a, b, c in ratio), flush=True)
         loose_fail = {k: (eh[k], e32[k]) for k in e32 if e32[k] > TOL and eh[k] > 2 * e32[k]}
         worst = sorted(eh.items(), key=lambda kv: -kv[1] / max(e32[kv[0]], TOL))[:12]
         out["variants"][v] = {"exact_fwd": fwd, "exact_bwd": bwd, "ms_fwd_bwd": ms,
@@ -159,7 +200,7 @@ def main():
               f"/{len(eh)}  strict_fail {len(strict_fail)} {sorted(strict_fail.items())[:6]}  "
               f"loose_fail {len(loose_fail)}  (oracle {time.time() - t1:.0f} s)", flush=True)
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-        with open(os.path.join(ROOT, "gpurun_out", "redweb_parity.json"), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", f"redweb_parity_{case}.json"), "w") as f:
             json.dump(out, f, indent=1)
 
 
