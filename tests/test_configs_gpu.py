@@ -30,7 +30,8 @@ restatement lands within 1e-3 (HIP global rel-L2 8.6e-5); the ff_effnet tests he
 flip-aware reference with the strict 1e-3 bar and report the plain comparison and the flip counts
 beside it. The ff_redweb tests are flip-aware at all 86 ReLU sites; their per-tensor bar comes from
 TWO fp32 restatements (oneDNN and native convolutions): 1e-3 wherever both are within 5e-4, else
-SPREAD (2.5) x the worse of the two (check_gradients' docstring has the measurements behind it).
+SPREAD (2.0) x the worse of the two, with one NAMED exception (FORWARD_ORIGIN) whose excess is
+traced to the forward activations and checked by decomposition instead (check_gradients).
 Every flip-aware test also checks that each HIP branch flip lies where the fp64 pre-activation is
 within rounding of 0 (FLIP_MARGIN), so a wrong forward branch cannot hide in the flip-aware
 reference.
@@ -96,7 +97,8 @@ def _nonuniform(drop):
 # the ff_effnet tests compare flip-aware with no exception.)
 
 
-def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None, second=None):
+def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None, second=None,
+                    exceptions=None):
     """The bar of the module docstring; returns the per-tensor report. g64_32: the fp64
     reference the fp32 restatement is measured against (default g64; the flip-aware form gives
     each implementation the fp64 gradient along its own ReLU branches). Per tensor: 1e-3
@@ -104,13 +106,12 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
     second = (g32b, g64_32b): a second fp32 restatement (the same semantics with torch's native
     convolutions instead of oneDNN: another summation order) and its flip-aware fp64 reference.
     With it the per-tensor bar follows how well-conditioned the tensor is by BOTH fp32
-    restatements: 1e-3 wherever both are within 1e-3 / 2, else SPREAD x the larger of their
-    errors (1e-3 floor). Why (ff_redweb at batch 32, profiles/r05_redweb_parity_*): the two fp32
-    restatements' per-tensor errors differ by up to 2.35x (median 0.87) and disagree about 1e-3
-    on 5 of 237 tensors; HIP's exact-fp32 path misses "1e-3 wherever the oneDNN restatement
-    meets it" on 2-3 tensors, and running the conv5 stage or the FFL convs exact fp32 changes
-    no HIP error by more than 2 %: single-sample closeness to 1e-3 is rounding-order noise."""
+    restatements: 1e-3 wherever both are within 1e-3 / 2, else SPREAD (2.0) x the larger of their
+    errors (1e-3 floor) — so wherever the two agree (within 1.5x, as they do on all but a few
+    tensors) HIP stays within 2x of both. exceptions = {tensor: (ok, note)}: tensors whose bar
+    is replaced by a check the caller made (FORWARD_ORIGIN); reported with both."""
     g64_32 = g64 if g64_32 is None else g64_32
+    exceptions = exceptions or {}
     keys = [k for k in g64 if not structural_zero(k)]
     rows, fails = {}, []
     for k in keys:
@@ -124,7 +125,12 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
             bar = TOL if worst <= TOL / 2 else max(TOL, SPREAD * worst)
             rows[k] = {"hip": e_hip, "fp32_restatement": e32, "fp32_restatement_native_conv": e32b,
                        "bar": bar}
-        if e_hip > bar:
+        if k in exceptions:
+            ok, note = exceptions[k]
+            rows[k]["exception"] = note
+            if not ok:
+                fails.append((k, e_hip, note))
+        elif e_hip > rows[k]["bar"]:
             fails.append((k, e_hip, e32))
     flat = lambda g: torch.cat([torch.as_tensor(g[k]).detach().double().cpu().flatten()
                                 for k in keys])
@@ -135,7 +141,8 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
             "tensors": len(keys),
             "tensors_fp32_within_1e-3": sum(r["fp32_restatement"] <= TOL for r in rows.values()),
             "tensors_hip_within_1e-3": sum(r["hip"] <= TOL for r in rows.values()),
-            "tensors_strict_bar": sum(r["bar"] <= TOL for r in rows.values())}
+            "tensors_strict_bar": sum(r["bar"] <= TOL for r in rows.values()),
+            "exceptions": sorted(exceptions)}
     if second is not None:
         d, e = flat(second[0]), flat(second[1])
         glob["fp32_native_conv_rel_l2"] = float((d - e).norm() / e.norm())
@@ -149,6 +156,69 @@ def check_gradients(tag, hip, g64, g32, structural_zero, g64_32=None, extra=None
     assert glob["hip_rel_l2"] <= max(TOL, 2.0 * glob["fp32_rel_l2"],
                                      2.0 * glob.get("fp32_native_conv_rel_l2", 0.0))
     return glob
+
+
+# A BN-gamma gradient is sum(dz * xhat) over the batch: where that sum cancels, the error of the
+# FORWARD activations xhat is amplified into it, and the pattern of that error (set by the chaotic
+# ResNet-50 encoder under training-mode BN: fp32 rounding of conv2-stage inputs grows ~100x by
+# conv5) decides how much. tools/exp_redweb_dz.py (round 6,
+# profiles/r06_redweb_dz.txt) traced the one ff_redweb tensor over 2x both fp32 restatements in
+# test_cfg3_redweb_448 (ffl2/block_down/bn3/gamma: HIP 1.52e-3, oneDNN 6.78e-4, native 6.71e-4,
+# ratio 2.24): with every decoder conv exact fp32, forward and backward, it moves < 1 %; fed the
+# same dL/dpred along the same ReLU branches, every HIP activation gradient of the decoder is
+# within 3.3e-5 of fp64, and the gamma gradient rebuilt from HIP's dz with fp64's xhat is 5.5e-4
+# from fp64 while HIP's dz with HIP's own xhat gives 1.85e-3 — the excess enters through xhat.
+# For these named BNs the test therefore checks the two halves instead of the sum: the gradient
+# from HIP's dz and fp64's xhat within the tensor's normal bar (HIP's backward arithmetic), and
+# HIP's forward xhat within 2x the fp32 restatement's own xhat error (HIP's forward arithmetic).
+FORWARD_ORIGIN = {"cfg3_redweb448_mixed": ("ffl2/block_down/bn3",)}
+
+
+def _bn_capture(store, names):
+    """An oracle/redweb.py _bn wrapper recording the pre-BN input of the named BNs."""
+    orig = OR._bn
+
+    def bn(P_, name, xx, eps):
+        if name in names:
+            store[name] = xx.detach()
+        return orig(P_, name, xx, eps)
+    return orig, bn
+
+
+def _xhat(xx, eps):
+    mu = xx.mean(dim=(0, 2, 3), keepdim=True)
+    var = ((xx - mu) ** 2).mean(dim=(0, 2, 3), keepdim=True)
+    return (xx - mu) / torch.sqrt(var + eps)
+
+
+def tensor_bar(k, g32, g64_32, second):
+    """check_gradients' per-tensor bar (with `second`) for tensor k."""
+    worst = max(rel(g32[k], g64_32[k]), rel(second[0][k], second[1][k]))
+    return TOL if worst <= TOL / 2 else max(TOL, SPREAD * worst)
+
+
+def forward_origin_checks(tag, eng, bn_in64, bn_in32, g64h, relu_masks, bars):
+    """{gamma tensor: (ok, note)} for FORWARD_ORIGIN[tag] (see there). bars: tensor -> its normal
+    per-tensor bar (check_gradients' rule)."""
+    out = {}
+    for name in FORWARD_ORIGIN.get(tag, ()):
+        bt, i = name.rsplit("/bn", 1)
+        i = int(i)
+        d = next(f for f in eng.ffls if bt.startswith(f["name"] + "/"))
+        bn = d["left" if "block_left" in bt else "down"]["bns"][i]
+        pre, site = f"{bt}/pre{i}", f"{bt}/act{i}"
+        xh_h = ((eng.act[pre].double() - bn.mean.double()) * bn.invstd.double()) \
+            .permute(0, 3, 1, 2).cpu()
+        xh_64 = _xhat(bn_in64[name].double(), OR.DEC_BN_EPS)
+        xh_32 = _xhat(bn_in32[name].double(), OR.DEC_BN_EPS)
+        dz_h = eng.gact[site].permute(0, 3, 1, 2).double().cpu() * relu_masks[site].double()
+        k = name + "/gamma"
+        e_bwd = rel((dz_h * xh_64).sum(dim=(0, 2, 3)), g64h[k])
+        e_xh, e_xh32 = rel(xh_h, xh_64), rel(xh_32, xh_64)
+        ok = e_bwd <= bars[k] and e_xh <= 2.0 * e_xh32
+        out[k] = (ok, {"gamma_from_hip_dz_fp64_xhat": e_bwd, "bar": bars[k],
+                       "hip_xhat": e_xh, "fp32_xhat": e_xh32})
+    return out
 
 
 def native_conv_restatement(O, P32, x32, dref32, P, x64, dref64, **kw):
@@ -217,11 +287,10 @@ def hip_decoder_relu_masks(eng, weights):
 FLIP_MARGIN = 2e-3  # observed (round 5): <= 3e-5 ff_effnet, 4.1e-4 ff_redweb at batch 2
 
 # Per-tensor factor over the worse fp32 restatement where a tensor is not clearly
-# well-conditioned (check_gradients' `second`): two exact-fp32 restatements of ff_redweb at batch
-# 32 differ per tensor by up to 2.35x (profiles/r05_redweb_parity_two_fp32.json), so a HIP error
-# within 2.5x of the worse one is inside the spread of fp32 summation orders. (Observed HIP /
-# worse-fp32 ratio: median 1.08, largest 2.24 on one of 237 tensors, cfg3 batch 2.)
-SPREAD = 2.5
+# well-conditioned (check_gradients' `second`). Round 5 set 2.5 after the one tensor at 2.24
+# (a bar fitted to the output); round 6 restores 2.0 and handles that tensor by name
+# with the decomposition check of FORWARD_ORIGIN.
+SPREAD = 2.0
 
 
 def flip_margin(z64, hip_mask):
@@ -462,9 +531,19 @@ def test_cfg3_redweb_448(cuda, fixed_schedules):
     taps, taps32 = {}, {}
     P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in weights.items()}
     b64, b32 = FlipProbe(mr), {}
-    with torch.no_grad():
-        pred_ref = OR.forward(P, x64, taps=taps, preprocessed=True, relu_branches=b64)
-        OR.forward(P32, torch.tensor(x), taps=taps32, preprocessed=True, relu_branches=b32)
+    tag = "cfg3_redweb448_mixed"
+    bn_in64, bn_in32 = {}, {}
+    named = FORWARD_ORIGIN.get(tag, ())
+    orig, cap64 = _bn_capture(bn_in64, named)
+    _, cap32 = _bn_capture(bn_in32, named)
+    try:
+        with torch.no_grad():
+            OR._bn = cap64
+            pred_ref = OR.forward(P, x64, taps=taps, preprocessed=True, relu_branches=b64)
+            OR._bn = cap32
+            OR.forward(P32, torch.tensor(x), taps=taps32, preprocessed=True, relu_branches=b32)
+    finally:
+        OR._bn = orig
     for name in ["conv1_relu", "conv2_block3_out", "conv3_block4_out", "conv4_block3_out",
                  "conv5_block3_out", "ffl0", "ffl1"]:
         mine = eng.act[name if not name.startswith("ffl") else name + "/out"]
@@ -488,10 +567,12 @@ def test_cfg3_redweb_448(cuda, fixed_schedules):
     second = native_conv_restatement(OR, P32, torch.tensor(x), dref.float(), P, x64, dref,
                                      preprocessed=True)
     zeros = {"aol/conv0/bias", "aol/conv1/bias", "aol/conv2/bias"}
-    check_gradients("cfg3_redweb448_mixed", {k: eng.grads[k] for k in g64h}, g64h, g32,
+    bars = {n + "/gamma": tensor_bar(n + "/gamma", g32, g64f, second) for n in named}
+    exc = forward_origin_checks(tag, eng, bn_in64, bn_in32, g64h, mr, bars)
+    check_gradients(tag, {k: eng.grads[k] for k in g64h}, g64h, g32,
                     lambda k: k in zeros, g64_32=g64f,
                     extra={"relu_flips_vs_fp64_total": flips, "flip_margin": dict(b64.margin),
-                           "flip_margin_check": margin}, second=second)
+                           "flip_margin_check": margin}, second=second, exceptions=exc)
 
 
 # ------------------------------------------------------------------- cfg5: full ListMLE
