@@ -51,9 +51,6 @@ struct GemmConvParams {
   int sk_nk, sk_tiles, sk_nnb, sk_align;
   float* sk_slab;
   int sk_q;  // steps per cut unit of a non-aligned range (0 / 1: any step)
-  // row-band halo kernel (conv_x3_halo.hip): workgroup order, 0 = N tiles fastest, 1 = M tiles
-  // fastest (the workgroups an XCD runs together share one filter panel)
-  int raster;
 };
 
 // first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)

@@ -28,12 +28,6 @@
 namespace pld {
 namespace x3 {
 
-#ifndef HALO_ABL
-#define HALO_ABL 0  // ablation builds (timing only, results garbage): 1 no MFMA, 2 no global
-#endif              // loads, 3 no K-loop barriers, 4 no consumer LDS reads, 5 no epilogue
-#ifndef HALO_PIPE
-#define HALO_PIPE 1
-#endif
 constexpr int HALO_WMAX = 56;
 constexpr int HALO_TAPS = 9;
 constexpr int HALO_PARTS = 8;  // a chunk's patch is staged in the first 8 of its 9 K-steps
@@ -118,8 +112,7 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
       const int row = e >> 3, c = chb + 4 * (e & 7);
       const int pix = ci.P0 + row;
       const bool ok = row < np && (unsigned)pix < (unsigned)npix && c < cs;
-      ra[i] = HALO_ABL == 2 ? make_float4(0.f, 0.f, 0.f, 0.f)
-                            : bload4(rs, ok ? (unsigned)((pix * cs + c) * 4) : OOB);
+      ra[i] = bload4(rs, ok ? (unsigned)((pix * cs + c) * 4) : OOB);
     }
   };
   auto store_part = [&](int buf, int t, const float4(&ra)[IAP]) {
@@ -151,8 +144,7 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
     for (int j = 0; j < FB; ++j) {
       const int nn = ci.n0 + pw * (BN / 4) + 8 * j + (br >> 2);
       const bool ok = kcin && nn < p.N;
-      rb[j] = HALO_ABL == 2 ? make_float4(0.f, 0.f, 0.f, 0.f)
-                            : bload4(rsb, ok ? ((unsigned)(nn * p.K + kc)) * 4u + 16u * half : OOB);
+      rb[j] = bload4(rsb, ok ? ((unsigned)(nn * p.K + kc)) * 4u + 16u * half : OOB);
     }
   };
   auto store_b = [&](int buf, const float4(&rb)[FB]) {
@@ -178,7 +170,10 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
     *reinterpret_cast<u32x4*>(A + S::ZR * 64 + 16 * (ptid & 3)) = u32x4{0u, 0u, 0u, 0u};
   }
   float4 pa[HALO_PARTS][IAP];  // the next unit's patch, in flight
-  float4 rb[2][FB];            // filter slabs, two in flight
+  // filter slabs in flight in registers (a divisor of 18, so that the stage is addressed at
+  // compile time; 3 and 6 measured no faster: the slabs are L2 hits)
+  constexpr int BD = 2;
+  float4 rb[BD][FB];
   // prologue: unit 0's patch and its first two filter slabs stored; unit 1's patch and slabs
   // 2, 3 in flight
   CI c0 = info(0), c1 = info(1), c2;
@@ -192,8 +187,8 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
   store_b(1, rb[1]);
 #pragma unroll
   for (int t = 0; t < HALO_PARTS; ++t) load_part(c1, t, pa[t]);
-  load_b(c0, 2, rb[0]);
-  load_b(c0, 3, rb[1]);
+#pragma unroll
+  for (int j = 0; j < BD; ++j) load_b(c0, 2 + j, rb[j]);
   lds_barrier();
   for (int c = 0; c < nunits; c += 2) {
 #pragma unroll
@@ -205,14 +200,14 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
         c2 = info(cc + 2);
       }
       const int i = HALO_TAPS * cc + t;
-      store_b((i + 2) % 3, rb[u & 1]);
-      if (t + 4 < HALO_TAPS) load_b(c0, t + 4, rb[u & 1]);  // step i + 4
-      else load_b(c1, t + 4 - HALO_TAPS, rb[u & 1]);
+      store_b((i + 2) % 3, rb[u % BD]);
+      if (t + 2 + BD < HALO_TAPS) load_b(c0, t + 2 + BD, rb[u % BD]);  // step i + 2 + BD
+      else load_b(c1, t + 2 + BD - HALO_TAPS, rb[u % BD]);
       if (t < HALO_PARTS) {
         store_part((cc + 1) & 1, t, pa[t]);
         load_part(c2, t, pa[t]);
       }
-      if (HALO_ABL != 3) lds_barrier();
+      lds_barrier();
     }
   }
 }
@@ -271,7 +266,6 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   // fragments of relative step i, k-half s: the patch of its unit shifted by its tap (a lane
   // whose tap leaves its image reads the zero row), its filter slab
   auto read = [&](int i, int s, Frags& f) {
-    if (HALO_ABL == 4) return;
     const int ci = i / HALO_TAPS, tap = i - ci * HALO_TAPS;
     const int ty = tap / 3;
     const int toff = ty * p.w + (tap - 3 * ty);
@@ -291,7 +285,6 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
     }
   };
   auto mma = [&](const Frags& f) {
-    if (HALO_ABL == 1) return;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -314,12 +307,6 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
     if constexpr (NM > NR * PER) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR * PER, 0);
   };
   Frags f0, f1;
-  if (HALO_ABL == 4) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a) f0.ah[a] = f0.al[a] = f1.ah[a] = f1.al[a] = bf16x8{};
-#pragma unroll
-    for (int b = 0; b < TN; ++b) f0.bh[b] = f0.bl[b] = f1.bh[b] = f1.bl[b] = bf16x8{};
-  }
   const int n = g_end - g_begin;
   // STREAM: the tile of the current unit, its first unit, the chunk within it
   const int u0 = g_begin / HALO_TAPS, u_end = g_end / HALO_TAPS;
@@ -332,7 +319,7 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   }
   setup(mb);
   lds_barrier();
-  if (!STREAM && HALO_PIPE) {
+  if constexpr (!STREAM) {
     if (n > 0) read(0, 0, f0);
     for (int i = 0; i < n; ++i) {
       read(i, 1, f1);  // the second half of this step while the first multiplies
@@ -349,12 +336,12 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       // no LDS drain before this barrier: the reads still in flight are the next step's, from
       // buffers the producers do not write in the coming iteration (filter buffer (i + 1) % 3,
       // the current or next unit's patch); this step's reads completed under its MFMAs
-      if (HALO_ABL != 3) {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
   } else {
+    // tile stream: one step at a time (reading the next step ahead would need the next tile's
+    // rows across a tile boundary)
     for (int i = 0; i < n; ++i) {
       read(i, 0, f0);
       __builtin_amdgcn_sched_barrier(0);
@@ -362,33 +349,30 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       read(i, 1, f0);
       __builtin_amdgcn_sched_barrier(0);
       mma(f0);
-      if constexpr (STREAM) {
-        // a tile's last step (or the range's): its sums out — whole tiles through the
-        // epilogue, a tile cut between workgroups as raw partials for the fixup kernel
-        if (i % HALO_TAPS == HALO_TAPS - 1) {
-          if (kq == p.kc_tap - 1 || i == n - 1) {
-            const int first = tile * p.kc_tap;
-            if (first >= u0 && first + p.kc_tap <= u_end)
-              store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane);
-            else
-              store_partial<TM, TN, BM, BN>(p, acc, wm * WTM, wn * WTN, lane, wid,
-                                            tile == u0 / p.kc_tap ? 0 : 1);
-            zero();
-            ++tile;
-            kq = 0;
-            mb = tile / p.sk_nnb;
-            nb = tile - mb * p.sk_nnb;
-            setup(mb);
-          } else {
-            ++kq;
-          }
+      // a tile's last step (or the range's): its sums out — whole tiles through the epilogue, a
+      // tile cut between workgroups as raw partials for the fixup kernel
+      if (i % HALO_TAPS == HALO_TAPS - 1) {
+        if (kq == p.kc_tap - 1 || i == n - 1) {
+          const int first = tile * p.kc_tap;
+          if (first >= u0 && first + p.kc_tap <= u_end)
+            store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane);
+          else
+            store_partial<TM, TN, BM, BN>(p, acc, wm * WTM, wn * WTN, lane, wid,
+                                          tile == u0 / p.kc_tap ? 0 : 1);
+          zero();
+          ++tile;
+          kq = 0;
+          mb = tile / p.sk_nnb;
+          nb = tile - mb * p.sk_nnb;
+          setup(mb);
+        } else {
+          ++kq;
         }
       }
-      if (HALO_ABL != 3) lds_barrier();
+      lds_barrier();
     }
   }
   if constexpr (STREAM) return;
-  if (HALO_ABL == 5) return;
   // epilogue (conv_x3_kernel's grid form): the staging buffers are free after the last barrier
   if constexpr (4 * 32 * (WTN + 8) * 4 <= S::BYTES) {
     if (staged_ok(p)) {
@@ -421,8 +405,8 @@ __global__ __launch_bounds__(512) void conv_x3_halo_kernel(GemmConvParams p) {
     kt_begin = (int)sk_begin(p, wid, nwg);
     kt_end = (int)sk_begin(p, wid + 1, nwg);
   } else {
-    nb = p.raster ? (wid / nmb) % nnb : wid % nnb;
-    mb = p.raster ? wid % nmb : (wid / nnb) % nmb;
+    nb = wid % nnb;  // (M tiles fastest instead measured no different)
+    mb = (wid / nnb) % nmb;
     zb = wid / (nnb * nmb);
     kt_begin = 0;
     kt_end = p.kc_tap * HALO_TAPS;
@@ -496,11 +480,6 @@ extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int s
     return PLD_ERR_ARG;
   }
   hipStream_t st = as_stream(stream);
-  static const int raster_env = [] {
-    const char* e = std::getenv("PLD_HALO_RASTER");
-    return e ? std::atoi(e) : 0;
-  }();
-  p->raster = raster_env;
   switch (cfg) {
     case 0: x3::halo_launch<256, 128, 2, 2>(*p, splits, sk_grid, st); break;
     case 1: x3::halo_launch<128, 256, 2, 2>(*p, splits, sk_grid, st); break;
