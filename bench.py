@@ -753,7 +753,10 @@ def run(a, world):
         same, sums = dp.replicas_identical(tr.engine.params.buf, pg)
         dist_check = {"replicas_identical": same, "param_checksums": sums,
                       "rccl_version": dp.rccl_version() if a.backend == "nccl" else None,
-                      "timeout_s": a.dist_timeout}
+                      "timeout_s": a.dist_timeout,
+                      # decoder buckets all-reduced while the encoder backward runs
+                      # (trainer dp_overlap; PLD_DP_OVERLAP=0: after the backward)
+                      "dp_overlap": tr.dp_overlap}
 
     # dominant conv kernel + conv family: algorithmic FLOPs / measured duration (HIP events on
     # the trainer's stream, one eager step)

@@ -527,7 +527,28 @@ class EffNetFF:
         return next(off for n, _, off in self.params.specs if n == name)
 
     def backward(self, dpred):
-        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params)."""
+        """Backward from d loss / d pred: fills self.grads (decoder kernels/biases, BN params).
+        The decoder chain (backward_decoder), its deferred weight gradients on the side stream
+        beside the encoder chain (backward_encoder), joined at the end."""
+        deferred = self.backward_decoder(dpred)
+        main = torch.cuda.current_stream(self.device)
+        if deferred:
+            wstream, fork = self._wgrad_side()
+            fork[-1].record(main)
+            with torch.cuda.stream(wstream):
+                wstream.wait_event(fork[-1])
+                for wg in deferred:
+                    wg()
+        self.backward_encoder()
+        if self.overlap_wgrad:  # join: every weight gradient is final on the caller's stream
+            main.wait_stream(self._wgrad_side()[0])
+
+    def backward_decoder(self, dpred):
+        """The decoder part of the backward on the current stream, down to the gradient of the
+        encoder's top activation. Returns the weight-gradient calls deferred for the side stream
+        (overlap_wgrad == 2; [] otherwise: run inline, or forked per layer in mode 1). Split out
+        so that the data-parallel trainer can all-reduce the decoder's gradients while the
+        encoder's backward runs (ReplicaTrainer.dp_overlap)."""
         A, G, B = self.act, self.gact, self.B
         a = K.conv_args
         h, w = self.H, self.W
@@ -595,13 +616,12 @@ class EffNetFF:
                 K.conv2d_wgrad(args, gpre, conv.dw)
                 K.channel_sum(gpre, rows, conv.cout, conv.db)
             K.conv2d_dgrad(args, gpre, conv.w_dg, g1, g2)  # skip grads: fresh write
-        if side and deferred:
-            fork[-1].record(main)
-            with torch.cuda.stream(wstream):
-                wstream.wait_event(fork[-1])
-                for wg in deferred:
-                    wg()
-        # encoder
+        return deferred if side else []
+
+    def backward_encoder(self):
+        """The encoder part of the backward (after backward_decoder) on the current stream."""
+        A, G, B = self.act, self.gact, self.B
+        a = K.conv_args
         h, w = A["top_pre"].shape[1:3]
         rows = B * h * w
         gpre = self._gpre_buf(A["top_pre"].shape)
@@ -616,8 +636,6 @@ class EffNetFF:
             self._block_bwd(blk, x_in, gx_in)
         rows = B * A["stem_pre"].shape[1] * A["stem_pre"].shape[2]
         self.stem_bn.bwd(A["stem_pre"], G["stem_activation"], rows, "swish", None)
-        if side:  # join: every weight gradient is final on the caller's stream from here
-            main.wait_stream(wstream)
 
     def _block_bwd(self, blk, x_in, gx_in):
         A, G, B, n = self.act, self.gact, self.B, blk["name"]

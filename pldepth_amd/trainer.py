@@ -37,9 +37,13 @@ class ReplicaTrainer:
     def __init__(self, input_shape=(448, 448, 3), batch_size=32, ranking_size=5,
                  rankings_per_image=100, sampling_type=1, seed=0, rank=0, world_size=1,
                  process_group=None, model="ff_effnet", drop_connect=True, engine=None,
-                 gpu_sampler=True, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+                 gpu_sampler=True, beta_1=0.9, beta_2=0.999, epsilon=1e-7, dp_overlap=None):
         """gpu_sampler=False: rankings come from the caller (set_rankings), as model.fit feeds
-        y_true batches; otherwise the GPU sampler draws them from (gt, mask) each step."""
+        y_true batches; otherwise the GPU sampler draws them from (gt, mask) each step.
+        dp_overlap (N > 1; default from PLD_DP_OVERLAP, on): all-reduce the decoder's gradient
+        buckets while the encoder's backward runs (engines with backward_decoder /
+        backward_encoder and deferred weight gradients; others take the post-backward
+        exchange)."""
         if engine is None and model not in ENGINES:
             raise ValueError(f"unknown model {model!r} (expected one of {sorted(ENGINES)})")
         self.gpu_sampler = gpu_sampler
@@ -80,6 +84,19 @@ class ReplicaTrainer:
         self.graphs = None
         self.stream = torch.cuda.Stream(device=dev)
         self.side = torch.cuda.Stream(device=dev)  # per-bucket optimizer updates (N > 1)
+        if dp_overlap is None:  # (an explicit True also serves a single-rank group: tests)
+            dp_overlap = world_size > 1 and os.environ.get("PLD_DP_OVERLAP", "1") == "1"
+        eng = self.engine
+        self.dp_overlap = bool(dp_overlap and hasattr(eng, "backward_decoder")
+                               and getattr(eng, "overlap_wgrad", 0) == 2)
+        if self.dp_overlap:
+            # the decoder's weight gradients and, after them, the decoder buckets' all-reduces
+            self.wside = torch.cuda.Stream(device=dev)
+            self._ev_dec = torch.cuda.Event()
+            # timing marks of the last overlapped step (tests): the first all-reduce issued on
+            # wside, the end of the encoder backward on the trainer stream
+            self._ev_ar = torch.cuda.Event(enable_timing=True)
+            self._ev_bwd = torch.cuda.Event(enable_timing=True)
 
     # ------------------------------------------------------------------ data
     def set_batch(self, images, gt, mask):
@@ -135,12 +152,15 @@ class ReplicaTrainer:
         K.sampler_rank(self.gt, self.valid_idx, self.nvalid, self.minmax, self.draws, self.R,
                        self.L, self.strategy, self.y_true)
 
-    def _fwd_bwd(self):
+    def _fwd_loss(self):
         eng = self.engine
         eng.forward(training=True, step=self.step_dev, image_offset=self.rank * self.B)
         K.listmle_fwd_bwd(eng.act["pred"], self.y_true, self.B, self.R_out, self.L,
                           dpred=self.dpred, nll=self.nll, loss=self.loss, zero_dpred=True)
-        eng.backward(self.dpred)
+
+    def _fwd_bwd(self):
+        self._fwd_loss()
+        self.engine.backward(self.dpred)
 
     def _update(self):
         eng = self.engine
@@ -199,9 +219,71 @@ class ReplicaTrainer:
         self.stream.wait_stream(self.side)
         K.step_increment(self.step_dev)
 
+    def _dp_decoder_split(self):
+        """Index of the first bucket holding an encoder tensor: buckets [0, split) hold only
+        decoder tensors (final once the decoder backward and its weight gradients are)."""
+        if not hasattr(self, "_dp_split"):
+            eng = self.engine
+            enc_hi = max((off + int(np.prod(shape)) for name, shape, off in eng.params.specs
+                          if not name.startswith(("dec_", "final"))), default=0)
+            bs = self._dp_buckets()
+            self._dp_split = next((i for i, (lo, hi) in enumerate(bs) if lo < enc_hi), len(bs))
+        return self._dp_split
+
+    def _dp_exchange_overlap(self, updates=None):
+        """dp_overlap: the decoder buckets' all-reduces issued on wside right behind the
+        decoder's weight gradients (the trainer stream meanwhile runs the encoder backward),
+        the encoder buckets' after the encoder backward on the trainer stream; each bucket's
+        update on the side stream as it lands (as _dp_exchange)."""
+        grads = self.engine.grads.buf
+        split = self._dp_decoder_split()
+        works = []
+        for i, (lo, hi) in enumerate(self._dp_buckets()):
+            if i < split:
+                with torch.cuda.stream(self.wside):
+                    if i == 0:
+                        self._ev_ar.record(self.wside)
+                    work = dp.allreduce_bucket(grads, lo, hi, self.pg)
+            else:
+                if i == split:
+                    self._ev_bwd.record(self.stream)
+                    self.side.wait_stream(self.stream)
+                work = dp.allreduce_bucket(grads, lo, hi, self.pg)
+            with torch.cuda.stream(self.side):
+                work.wait()
+                if updates is None:
+                    self._dp_update(lo, hi)
+                else:
+                    updates[i].launch()
+            works.append(work)
+        if split == len(works):
+            self._ev_bwd.record(self.stream)
+        self._dp_works = works
+        self.stream.wait_stream(self.side)
+        self.stream.wait_stream(self.wside)
+        K.step_increment(self.step_dev)
+
+    def _launch_deferred(self, deferred=None, graph=None):
+        """The decoder's deferred weight gradients on wside, after the decoder chain."""
+        self._ev_dec.record(self.stream)
+        self.wside.wait_event(self._ev_dec)
+        with torch.cuda.stream(self.wside):
+            if graph is not None:
+                graph.launch()
+            else:
+                for wg in deferred:
+                    wg()
+
     def _step_dp(self):
         """One data-parallel step (N > 1), eager, on self.stream (+ RCCL and the side stream)."""
         self._sample()
+        if self.dp_overlap:
+            self._fwd_loss()
+            deferred = self.engine.backward_decoder(self.dpred)
+            self._launch_deferred(deferred)
+            self.engine.backward_encoder()
+            self._dp_exchange_overlap()
+            return
         self._fwd_bwd()
         self._dp_exchange()
 
@@ -213,18 +295,36 @@ class ReplicaTrainer:
         RCCL's own stream, c10d's stream dependencies and work objects run as they do eagerly).
         Per step the host issues 1 + 2 x buckets launches and the collectives."""
         torch.cuda.synchronize()
-        with torch.cuda.stream(self.stream):
-            step = K.Graph().capture(lambda: (self._sample(), self._fwd_bwd()))
+        if self.dp_overlap:
+            # three compute graphs: sampler -> forward -> ListMLE -> decoder backward; the
+            # decoder's weight gradients (captured on wside); the encoder backward
+            dec = []
+            with torch.cuda.stream(self.stream):
+                g1 = K.Graph().capture(lambda: (self._sample(), self._fwd_loss(),
+                                                dec.extend(self.engine.backward_decoder(self.dpred))))
+            with torch.cuda.stream(self.wside):
+                gw = K.Graph().capture(lambda: [wg() for wg in dec])
+            with torch.cuda.stream(self.stream):
+                g2 = K.Graph().capture(self.engine.backward_encoder)
+            graphs = [g1, gw, g2]
+        else:
+            with torch.cuda.stream(self.stream):
+                graphs = [K.Graph().capture(lambda: (self._sample(), self._fwd_bwd()))]
         with torch.cuda.stream(self.side):
             upd = [K.Graph().capture(lambda lo=lo, hi=hi: self._dp_update(lo, hi))
                    for lo, hi in self._dp_buckets()]
         torch.cuda.synchronize()
-        self.graphs = [step]
+        self.graphs = graphs
         self.bucket_graphs = upd
 
     def _replay_dp(self):
         """One captured N > 1 step on self.stream (the caller's current stream)."""
         self.graphs[0].launch()
+        if self.dp_overlap:
+            self._launch_deferred(graph=self.graphs[1])
+            self.graphs[2].launch()
+            self._dp_exchange_overlap(self.bucket_graphs)
+            return
         self._dp_exchange(self.bucket_graphs)
 
     # ------------------------------------------------------------------ driving

@@ -5,7 +5,10 @@ Each rank owns half of a global batch of 4 and steps with the per-bucket all-red
 step 1 eager (trainer._step_dp), step 2 replayed from the capture (trainer._capture_dp /
 _replay_dp). After 2 steps its parameters must equal a single-process run that
 computes both shards' gradients, sums them and applies Adam with grad_scale 1/2 — the mean of the
-replica gradients, per-replica BN statistics (MirroredStrategy semantics)."""
+replica gradients, per-replica BN statistics (MirroredStrategy semantics).
+ff_effnet also runs the overlapped exchange (trainer dp_overlap: the decoder buckets all-reduced
+while the encoder backward runs), with the event-timestamp check that the first bucket's
+all-reduce was issued before the backward ended; ff_redweb keeps the post-backward exchange."""
 import os
 import socket
 
@@ -34,7 +37,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, port, q, model):
+def _rank_main(rank, port, q, model, overlap):
     import torch.distributed as dist
     from pldepth_amd import kernels as K
     from pldepth_amd.trainer import ReplicaTrainer
@@ -47,7 +50,8 @@ def _rank_main(rank, port, q, model):
         x, gt, mask = _data()
         sl = slice(rank * B, (rank + 1) * B)
         tr = ReplicaTrainer((H, H, 3), B, L, R, 1, seed=0, rank=rank, world_size=2,
-                            process_group=dist.group.WORLD, model=model)
+                            process_group=dist.group.WORLD, model=model, dp_overlap=overlap)
+        assert tr.dp_overlap == (overlap and model == "ff_effnet")
         tr.set_batch(torch.from_numpy(x[sl]).cuda(), torch.from_numpy(gt[sl]).cuda(),
                      torch.from_numpy(mask[sl]).cuda())
         tr.step_eager(0.01)
@@ -59,24 +63,36 @@ def _rank_main(rank, port, q, model):
         for _ in range(STEPS - 1):
             tr.step(0.01)
         tr.synchronize()
+        # dp_overlap: the first (decoder) bucket's all-reduce was issued on wside before the
+        # encoder backward ended on the trainer stream (event timestamps of the replayed step)
+        lead = None
+        if tr.dp_overlap:
+            torch.cuda.synchronize()
+            lead = tr._ev_ar.elapsed_time(tr._ev_bwd)
+            assert tr._dp_decoder_split() >= 1
         q.put((rank, (tr.engine.params.buf.cpu().numpy(), g1, p1), tr.loss_value(),
-               int(tr.step_dev.item())))
+               int(tr.step_dev.item()), lead))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["ff_effnet", "ff_redweb"])
-def test_world2_overlapped_step_equals_serial_mean(cuda, model):
+@pytest.mark.parametrize("model,overlap", [("ff_effnet", True), ("ff_effnet", False),
+                                           ("ff_redweb", True)])
+def test_world2_overlapped_step_equals_serial_mean(cuda, model, overlap):
     import torch.multiprocessing as mp
     from pldepth_amd import kernels as K
     from pldepth_amd.trainer import ReplicaTrainer
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, port, q, model)) for r in range(2)]
+    ps = [ctx.Process(target=_rank_main, args=(r, port, q, model, overlap)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict((r, (pb, lo, st)) for r, pb, lo, st in (q.get(timeout=240) for _ in ps))
+    out = {}
+    for r, pb, lo, st, lead in (q.get(timeout=240) for _ in ps):
+        if lead is not None:  # dp_overlap: ev_ar (first all-reduce issued) before ev_bwd
+            assert lead > 0, f"decoder all-reduce issued {-lead:.3f} ms after the backward ended"
+        out[r] = (pb, lo, st)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0

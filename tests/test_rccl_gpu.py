@@ -1,7 +1,9 @@
 """The data-parallel ReplicaTrainer path over the real "nccl" backend (= RCCL) on the one leased
 GPU: a single-rank RCCL process group, so RCCL's communicator, its own stream and c10d's stream
 dependencies (the side stream's work.wait() on RCCL's stream, then each bucket's Adam) run for
-real; the multi-rank tests (test_dp_gpu.py) need gloo because RCCL takes one GPU per rank.
+real — with the overlapped exchange (ff_effnet) also the all-reduces issued from the weight-
+gradient stream while the encoder backward replays; the multi-rank tests (test_dp_gpu.py) need
+gloo because RCCL takes one GPU per rank.
 
 The rank steps through the N > 1 machinery (trainer._step_dp eager, then _capture_dp /
 _replay_dp: compute graph, per-bucket all-reduces issued between the update graphs). With one
@@ -35,7 +37,7 @@ def _free_port():
     return p
 
 
-def _rank_main(port, q, model):
+def _rank_main(port, q, model, overlap):
     import torch.distributed as dist
     from pldepth_amd import kernels as K
     from pldepth_amd.trainer import ReplicaTrainer
@@ -48,7 +50,8 @@ def _rank_main(port, q, model):
     try:
         x, gt, mask = _data()
         tr = ReplicaTrainer((H, H, 3), B, L, R, 1, seed=0, rank=0, world_size=1,
-                            process_group=dist.group.WORLD, model=model)
+                            process_group=dist.group.WORLD, model=model, dp_overlap=overlap)
+        assert tr.dp_overlap == overlap
         tr.set_batch(torch.from_numpy(x).cuda(), torch.from_numpy(gt).cuda(),
                      torch.from_numpy(mask).cuda())
         with torch.cuda.stream(tr.stream):
@@ -74,14 +77,17 @@ def _rank_main(port, q, model):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["ff_effnet", "ff_redweb"])
-def test_rccl_single_rank_dp_step_equals_n1_step(cuda, model):
+@pytest.mark.parametrize("model,overlap", [("ff_effnet", False), ("ff_effnet", True),
+                                           ("ff_redweb", False)])
+def test_rccl_single_rank_dp_step_equals_n1_step(cuda, model, overlap):
+    """overlap: the decoder buckets' all-reduces issued on RCCL from the weight-gradient stream
+    while the encoder backward runs (trainer dp_overlap), as the driver's 8-GPU run does."""
     import torch.multiprocessing as mp
     from pldepth_amd import kernels as K
     from pldepth_amd.trainer import ReplicaTrainer
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rank_main, args=(_free_port(), q, model))
+    p = ctx.Process(target=_rank_main, args=(_free_port(), q, model, overlap))
     p.start()
     backend, version, nbuckets, pb, g1, p1, loss, step = q.get(timeout=240)
     p.join(timeout=60)
