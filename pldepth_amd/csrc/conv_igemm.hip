@@ -929,6 +929,7 @@ extern "C" int pld__x3_patch_wgrad_th(int N);
 extern "C" int pld__x3_num_halo(void);
 extern "C" int pld__x3_halo_dims(int cfg, int* bm, int* bn, int* tm, int* tn);
 extern "C" int pld__x3_halo_ok(const GemmConvParams* p);
+extern "C" int pld__x3_halo_wmax(int cfg);
 extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int sk_grid,
                                    void* stream);
 extern "C" int pld__x3_halo_stream_plan(GemmConvParams* p, int cfg);
@@ -1143,7 +1144,8 @@ static int run_fwd_gemm(GemmConvParams& p, bool vec, bool vec16, int tile, void*
   bool patch, stream, halo;
   resolve_sched(math, x3_fwd_geom(p.C, p.c1, p.in_scale != nullptr, p.kh * p.kw), tile, x3,
                 tile, &patch, &stream, &halo);
-  if (halo && !pld__x3_halo_ok(&p)) {  // halo schedule on another shape: default tile
+  if (halo && (!pld__x3_halo_ok(&p) || p.w > pld__x3_halo_wmax(tile % pld__x3_num_halo()))) {
+    // halo schedule on another shape (or a map wider than it takes): default tile
     halo = false;
     tile = -1;
   }
@@ -1546,8 +1548,9 @@ extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
     case PLD_SCHED_X3_HALO: {
       const int h = idx - x3_halo_base(), nh = pld__x3_num_halo();
       pld__x3_halo_dims(h % nh, &bm, &bn, &tm, &tn);
-      snprintf(out, 24, "%s/%dx%d", h < nh ? "x3halo" : h < 2 * nh ? "x3halosplit" : "x3halostream",
-               bm, bn);
+      // maps up to 28 wide, two workgroups per CU: "x3halo28..."
+      snprintf(out, 24, "x3halo%s%s/%dx%d", pld__x3_halo_wmax(h % nh) == 28 ? "28" : "",
+               h < nh ? "" : h < 2 * nh ? "split" : "stream", bm, bn);
       break;
     }
     default: {
@@ -1605,8 +1608,9 @@ extern "C" const char* pld_conv_kernel_name(const pld_conv_args* a, int mode) {
     const int c1 = mode == 0 ? a->c1 : a->cout, c2 = mode == 0 ? a->c2 : 0;
     const int w = mode == 0 ? a->w : a->ow, h = mode == 0 ? a->h : a->oh;
     const int ow = mode == 0 ? a->ow : a->w, oh = mode == 0 ? a->oh : a->h;
+    const int wmax = pld__x3_halo_wmax((a->tile - x3_halo_base()) % pld__x3_num_halo());
     const bool ok = a->kh == 3 && a->kw == 3 && a->sh == 1 && a->sw == 1 && a->in_scale == nullptr &&
-                    oh == h && ow == w && w <= 56 && c1 % 8 == 0 && c2 % 8 == 0 &&
+                    oh == h && ow == w && w <= wmax && c1 % 8 == 0 && c2 % 8 == 0 &&
                     a->pad_t >= 0 && a->pad_t <= 2 && a->pad_l >= 0 && a->pad_l <= 2;
     return ok ? "conv_x3_halo_kernel" : "conv_x3_kernel";
   }

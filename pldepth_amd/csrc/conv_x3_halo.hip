@@ -32,15 +32,19 @@ constexpr int HALO_WMAX = 56;
 constexpr int HALO_TAPS = 9;
 constexpr int HALO_PARTS = 8;  // a chunk's patch is staged in the first 8 of its 9 K-steps
 
-template <int BM, int BN>
+// WMAX: widest map an instantiation takes; NB: filter slab buffers (3: the consumers read the
+// next step's first fragments under the current step's MFMAs; 2: one step at a time, the LDS
+// of two resident workgroups per CU, so that one's prologue / epilogue hides under the other's
+// MFMAs — the short-K dgrads)
+template <int BM, int BN, int WMAX = HALO_WMAX, int NB = 3>
 struct HaloSmem {
-  static constexpr int NPMAX = BM + 2 * HALO_WMAX + 2;  // patch rows of the widest map
+  static constexpr int NPMAX = BM + 2 * WMAX + 2;  // patch rows of the widest map
   static constexpr int ZR = NPMAX;                       // the zero row (after the patch rows)
   static constexpr int A_PLANE = (NPMAX + 1) * 64;       // [row][32 k] bf16, chunk_off layout
   static constexpr int A_BYTES = 2 * A_PLANE;            // hi + lo
   static constexpr int B_PLANE = BN * 64;
   static constexpr int B_BYTES = 2 * B_PLANE;
-  static constexpr int BYTES = 2 * A_BYTES + 3 * B_BYTES;
+  static constexpr int BYTES = 2 * A_BYTES + NB * B_BYTES;
   __device__ static unsigned char* a(unsigned char* s, int buf) { return s + buf * A_BYTES; }
   __device__ static unsigned char* b(unsigned char* s, int buf) {
     return s + 2 * A_BYTES + buf * B_BYTES;
@@ -52,11 +56,12 @@ struct HaloSmem {
 // (mb, nb), units = its chunks [g_begin / 9, g_end / 9). STREAM: global units u = tile x kc_tap
 // + chunk over the tile-major stream, the workgroup's range cut on unit boundaries (sk_begin,
 // sk_q = 9); a range may end and start mid-tile.
-template <int BM, int BN, bool CAT, bool STREAM>
+template <int BM, int BN, bool CAT, bool STREAM, int WMAX, int NB>
 __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned char* smem,
                                               int g_begin, int g_end, int pw, int lane, int mb0,
                                               int nb0) {
-  using S = HaloSmem<BM, BN>;
+  using S = HaloSmem<BM, BN, WMAX, NB>;
+  constexpr int LEAD = NB - 1;  // K-steps the stored filter slab runs ahead of the consumers
   const int ptid = pw * 64 + lane;
   const int n = g_end - g_begin;
   if (n <= 0) {  // barriers: 1 + n, matching the consumers
@@ -179,16 +184,16 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
   CI c0 = info(0), c1 = info(1), c2;
 #pragma unroll
   for (int t = 0; t < HALO_PARTS; ++t) load_part(c0, t, pa[t]);
-  load_b(c0, 0, rb[0]);
-  load_b(c0, 1, rb[1]);
+#pragma unroll
+  for (int j = 0; j < LEAD; ++j) load_b(c0, j, rb[j]);
 #pragma unroll
   for (int t = 0; t < HALO_PARTS; ++t) store_part(0, t, pa[t]);
-  store_b(0, rb[0]);
-  store_b(1, rb[1]);
+#pragma unroll
+  for (int j = 0; j < LEAD; ++j) store_b(j, rb[j]);
 #pragma unroll
   for (int t = 0; t < HALO_PARTS; ++t) load_part(c1, t, pa[t]);
 #pragma unroll
-  for (int j = 0; j < BD; ++j) load_b(c0, 2 + j, rb[j]);
+  for (int j = 0; j < BD; ++j) load_b(c0, LEAD + j, rb[j]);
   lds_barrier();
   for (int c = 0; c < nunits; c += 2) {
 #pragma unroll
@@ -200,9 +205,9 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
         c2 = info(cc + 2);
       }
       const int i = HALO_TAPS * cc + t;
-      store_b((i + 2) % 3, rb[u % BD]);
-      if (t + 2 + BD < HALO_TAPS) load_b(c0, t + 2 + BD, rb[u % BD]);  // step i + 2 + BD
-      else load_b(c1, t + 2 + BD - HALO_TAPS, rb[u % BD]);
+      store_b((i + LEAD) % NB, rb[u % BD]);
+      if (t + LEAD + BD < HALO_TAPS) load_b(c0, t + LEAD + BD, rb[u % BD]);  // step i+LEAD+BD
+      else load_b(c1, t + LEAD + BD - HALO_TAPS, rb[u % BD]);
       if (t < HALO_PARTS) {
         store_part((cc + 1) & 1, t, pa[t]);
         load_part(c2, t, pa[t]);
@@ -213,11 +218,11 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
 }
 
 // ---------------------------------------------------------------------------- consumer
-template <int BM, int BN, int WM, int WN, bool STREAM>
+template <int BM, int BN, int WM, int WN, bool STREAM, int WMAX, int NB>
 __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned char* smem,
                                               int g_begin, int g_end, int wave, int lane, int mb,
                                               int nb, int zb, int wid) {
-  using S = HaloSmem<BM, BN>;
+  using S = HaloSmem<BM, BN, WMAX, NB>;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   const int wm = wave / WN, wn = wave % WN;
@@ -270,7 +275,7 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
     const int ty = tap / 3;
     const int toff = ty * p.w + (tap - 3 * ty);
     const unsigned char* A = S::a(smem, ci & 1);
-    const unsigned char* B = S::b(smem, i % 3);
+    const unsigned char* B = S::b(smem, i % NB);
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
       const int r = ((vm[a] >> tap) & 1u) ? pr[a] + toff : S::ZR;
@@ -319,7 +324,7 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   }
   setup(mb);
   lds_barrier();
-  if constexpr (!STREAM) {
+  if constexpr (!STREAM && NB == 3) {
     if (n > 0) read(0, 0, f0);
     for (int i = 0; i < n; ++i) {
       read(i, 1, f1);  // the second half of this step while the first multiplies
@@ -340,8 +345,8 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       asm volatile("" ::: "memory");
     }
   } else {
-    // tile stream: one step at a time (reading the next step ahead would need the next tile's
-    // rows across a tile boundary)
+    // one step at a time (the tile stream: reading the next step ahead would need the next
+    // tile's rows across a tile boundary; NB == 2: the next filter slab is not there yet)
     for (int i = 0; i < n; ++i) {
       read(i, 0, f0);
       __builtin_amdgcn_sched_barrier(0);
@@ -351,7 +356,7 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       mma(f0);
       // a tile's last step (or the range's): its sums out — whole tiles through the epilogue, a
       // tile cut between workgroups as raw partials for the fixup kernel
-      if (i % HALO_TAPS == HALO_TAPS - 1) {
+      if (STREAM && i % HALO_TAPS == HALO_TAPS - 1) {
         if (kq == p.kc_tap - 1 || i == n - 1) {
           const int first = tile * p.kc_tap;
           if (first >= u0 && first + p.kc_tap <= u_end)
@@ -386,12 +391,13 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane, zb);
 }
 
-template <int BM, int BN, int WM, int WN, bool CAT, bool STREAM>
-__global__ __launch_bounds__(512) void conv_x3_halo_kernel(GemmConvParams p) {
+template <int BM, int BN, int WM, int WN, bool CAT, bool STREAM, int WMAX, int NB>
+__global__ __launch_bounds__(512, NB == 2 ? 2 : 1) void conv_x3_halo_kernel(GemmConvParams p) {
+  using S = HaloSmem<BM, BN, WMAX, NB>;
   static_assert(WM * WN == 4, "4 consumer waves");
   static_assert((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0 && BN % 32 == 0, "wave tile");
-  static_assert(HaloSmem<BM, BN>::BYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[HaloSmem<BM, BN>::BYTES];
+  static_assert(S::BYTES <= (NB == 2 ? 80 : 160) * 1024, "LDS (NB == 2: two workgroups per CU)");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S::BYTES];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int nmb = gridDim.x, nnb = gridDim.y;
@@ -416,32 +422,36 @@ __global__ __launch_bounds__(512) void conv_x3_halo_kernel(GemmConvParams p) {
     }
   }
   if (wave >= 4)
-    halo_producer<BM, BN, CAT, STREAM>(p, smem, kt_begin, kt_end, wave - 4, lane, mb, nb);
+    halo_producer<BM, BN, CAT, STREAM, WMAX, NB>(p, smem, kt_begin, kt_end, wave - 4, lane, mb,
+                                                 nb);
   else
-    halo_consumer<BM, BN, WM, WN, STREAM>(p, smem, kt_begin, kt_end, wave, lane, mb, nb, zb,
-                                          wid);
+    halo_consumer<BM, BN, WM, WN, STREAM, WMAX, NB>(p, smem, kt_begin, kt_end, wave, lane, mb,
+                                                    nb, zb, wid);
 }
 
-// schedules: tile and consumer-wave grid
-struct HaloCfg { int bm, bn, wm, wn; };
+// schedules: tile, consumer-wave grid, widest map, filter slab buffers
+struct HaloCfg { int bm, bn, wm, wn, wmax, nb; };
 inline constexpr HaloCfg kHalo[] = {
-    {256, 128, 2, 2}, {128, 256, 2, 2}, {128, 128, 2, 2}, {256, 64, 4, 1}, {128, 160, 4, 1},
+    {256, 128, 2, 2, HALO_WMAX, 3}, {128, 256, 2, 2, HALO_WMAX, 3}, {128, 128, 2, 2, HALO_WMAX, 3},
+    {256, 64, 4, 1, HALO_WMAX, 3},  {128, 160, 4, 1, HALO_WMAX, 3},
+    // two workgroups per CU on maps up to 28 wide (the 28^2 / 14^2 decoder and ResNet convs)
+    {128, 128, 2, 2, 28, 2},        {128, 64, 2, 2, 28, 2},
 };
 constexpr int kNumHalo = (int)(sizeof(kHalo) / sizeof(kHalo[0]));
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int WMAX, int NB>
 static void halo_launch(GemmConvParams& p, int splits, int sk_grid, hipStream_t st) {
   if (sk_grid > 0) {  // tile stream (+ the fixup of the tiles cut between workgroups)
     const dim3 grid(sk_grid);
-    if (p.c2) conv_x3_halo_kernel<BM, BN, WM, WN, true, true><<<grid, 512, 0, st>>>(p);
-    else conv_x3_halo_kernel<BM, BN, WM, WN, false, true><<<grid, 512, 0, st>>>(p);
+    if (p.c2) conv_x3_halo_kernel<BM, BN, WM, WN, true, true, WMAX, NB><<<grid, 512, 0, st>>>(p);
+    else conv_x3_halo_kernel<BM, BN, WM, WN, false, true, WMAX, NB><<<grid, 512, 0, st>>>(p);
     if (!p.sk_align)
       x3_stream_fixup_kernel<BM, BN, WM><<<dim3(sk_grid, WM), 256, 0, st>>>(p, sk_grid);
     return;
   }
   const dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN), splits);
-  if (p.c2) conv_x3_halo_kernel<BM, BN, WM, WN, true, false><<<grid, 512, 0, st>>>(p);
-  else conv_x3_halo_kernel<BM, BN, WM, WN, false, false><<<grid, 512, 0, st>>>(p);
+  if (p.c2) conv_x3_halo_kernel<BM, BN, WM, WN, true, false, WMAX, NB><<<grid, 512, 0, st>>>(p);
+  else conv_x3_halo_kernel<BM, BN, WM, WN, false, false, WMAX, NB><<<grid, 512, 0, st>>>(p);
 }
 
 }  // namespace x3
@@ -450,6 +460,10 @@ static void halo_launch(GemmConvParams& p, int splits, int sk_grid, hipStream_t 
 using namespace pld;
 
 extern "C" int pld__x3_num_halo(void) { return x3::kNumHalo; }
+// the widest input map schedule cfg takes (0: no such schedule)
+extern "C" int pld__x3_halo_wmax(int cfg) {
+  return cfg >= 0 && cfg < x3::kNumHalo ? x3::kHalo[cfg].wmax : 0;
+}
 extern "C" int pld__x3_halo_dims(int cfg, int* bm, int* bn, int* tm, int* tn) {
   if (cfg < 0 || cfg >= x3::kNumHalo) return PLD_ERR_ARG;
   const x3::HaloCfg& c = x3::kHalo[cfg];
@@ -472,7 +486,8 @@ extern "C" int pld__x3_halo_ok(const GemmConvParams* p) {
 // stream, planned by pld__x3_halo_stream_plan) are the caller's (pld's run_fwd_gemm)
 extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int sk_grid,
                                    void* stream) {
-  if (!pld__x3_halo_ok(p) || cfg < 0 || cfg >= x3::kNumHalo || !p->bsplit || splits < 1 ||
+  if (!pld__x3_halo_ok(p) || cfg < 0 || cfg >= x3::kNumHalo || p->w > x3::kHalo[cfg].wmax ||
+      !p->bsplit || splits < 1 ||
       p->kc_tap <= 0 || (p->ktiles_per_split % x3::HALO_TAPS) != 0 ||
       (sk_grid > 0 && (p->sk_nk != p->kc_tap * x3::HALO_TAPS || p->sk_q != x3::HALO_TAPS ||
                        p->sk_tiles <= 0 || (!p->sk_align && !p->sk_slab)))) {
@@ -481,11 +496,13 @@ extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int s
   }
   hipStream_t st = as_stream(stream);
   switch (cfg) {
-    case 0: x3::halo_launch<256, 128, 2, 2>(*p, splits, sk_grid, st); break;
-    case 1: x3::halo_launch<128, 256, 2, 2>(*p, splits, sk_grid, st); break;
-    case 2: x3::halo_launch<128, 128, 2, 2>(*p, splits, sk_grid, st); break;
-    case 3: x3::halo_launch<256, 64, 4, 1>(*p, splits, sk_grid, st); break;
-    default: x3::halo_launch<128, 160, 4, 1>(*p, splits, sk_grid, st); break;
+    case 0: x3::halo_launch<256, 128, 2, 2, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
+    case 1: x3::halo_launch<128, 256, 2, 2, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
+    case 2: x3::halo_launch<128, 128, 2, 2, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
+    case 3: x3::halo_launch<256, 64, 4, 1, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
+    case 4: x3::halo_launch<128, 160, 4, 1, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
+    case 5: x3::halo_launch<128, 128, 2, 2, 28, 2>(*p, splits, sk_grid, st); break;
+    default: x3::halo_launch<128, 64, 2, 2, 28, 2>(*p, splits, sk_grid, st); break;
   }
   return check_launch("conv_x3_halo_kernel");
 }
@@ -501,7 +518,8 @@ extern "C" int pld__x3_halo_stream_plan(GemmConvParams* p, int cfg) {
   p->sk_tiles = (int)tiles;
   p->sk_nnb = (int)cdiv(p->N, bn);
   p->sk_q = x3::HALO_TAPS;
-  const long G = std::max<long>(1, std::min<long>(256, units / 4));
+  const long G = std::max<long>(1, std::min<long>(256L * (x3::kHalo[cfg].nb == 2 ? 2 : 1),
+                                                  units / 4));
   p->sk_align = (tiles % G == 0) ? 1 : 0;
   return (int)G;
 }

@@ -388,7 +388,8 @@ def _schedules(mode, math, a=None):
             continue
         if c == 2 and (a is None or not _patch_ok(mode, a)):
             continue
-        if c == 6 and (a is None or not _halo_ok(mode, a)):
+        if c == 6 and (a is None or not _halo_ok(mode, a)
+                       or ("halo28" in schedule_desc(math, i) and a.w > 28)):
             continue
         out.append(i)
     return out
