@@ -930,6 +930,7 @@ extern "C" int pld__x3_num_halo(void);
 extern "C" int pld__x3_halo_dims(int cfg, int* bm, int* bn, int* tm, int* tn);
 extern "C" int pld__x3_halo_ok(const GemmConvParams* p);
 extern "C" int pld__x3_halo_wmax(int cfg);
+extern "C" int pld__x3_halo_occ2(int cfg);
 extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int sk_grid,
                                    void* stream);
 extern "C" int pld__x3_halo_stream_plan(GemmConvParams* p, int cfg);
@@ -1548,8 +1549,9 @@ extern "C" const char* pld_conv_schedule_desc(int math, int idx) {
     case PLD_SCHED_X3_HALO: {
       const int h = idx - x3_halo_base(), nh = pld__x3_num_halo();
       pld__x3_halo_dims(h % nh, &bm, &bn, &tm, &tn);
-      // maps up to 28 wide, two workgroups per CU: "x3halo28..."
-      snprintf(out, 24, "x3halo%s%s/%dx%d", pld__x3_halo_wmax(h % nh) == 28 ? "28" : "",
+      // two workgroups per CU: "x3halo28..." (maps up to 28 wide), "x3halo2..." (up to 56)
+      const int wm = pld__x3_halo_wmax(h % nh), two = pld__x3_halo_occ2(h % nh);
+      snprintf(out, 24, "x3halo%s%s/%dx%d", wm == 28 ? "28" : two ? "2" : "",
                h < nh ? "" : h < 2 * nh ? "split" : "stream", bm, bn);
       break;
     }

@@ -436,6 +436,8 @@ inline constexpr HaloCfg kHalo[] = {
     {256, 64, 4, 1, HALO_WMAX, 3},  {128, 160, 4, 1, HALO_WMAX, 3},
     // two workgroups per CU on maps up to 28 wide (the 28^2 / 14^2 decoder and ResNet convs)
     {128, 128, 2, 2, 28, 2},        {128, 64, 2, 2, 28, 2},
+    // ... and up to 56 wide (smaller tiles: the 56^2 band is BM + 114 rows)
+    {128, 64, 2, 2, HALO_WMAX, 2},  {64, 128, 2, 2, HALO_WMAX, 2},
 };
 constexpr int kNumHalo = (int)(sizeof(kHalo) / sizeof(kHalo[0]));
 
@@ -463,6 +465,10 @@ extern "C" int pld__x3_num_halo(void) { return x3::kNumHalo; }
 // the widest input map schedule cfg takes (0: no such schedule)
 extern "C" int pld__x3_halo_wmax(int cfg) {
   return cfg >= 0 && cfg < x3::kNumHalo ? x3::kHalo[cfg].wmax : 0;
+}
+// 1: two workgroups per CU (double-buffered filter slab)
+extern "C" int pld__x3_halo_occ2(int cfg) {
+  return cfg >= 0 && cfg < x3::kNumHalo && x3::kHalo[cfg].nb == 2;
 }
 extern "C" int pld__x3_halo_dims(int cfg, int* bm, int* bn, int* tm, int* tn) {
   if (cfg < 0 || cfg >= x3::kNumHalo) return PLD_ERR_ARG;
@@ -502,7 +508,9 @@ extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int s
     case 3: x3::halo_launch<256, 64, 4, 1, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
     case 4: x3::halo_launch<128, 160, 4, 1, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
     case 5: x3::halo_launch<128, 128, 2, 2, 28, 2>(*p, splits, sk_grid, st); break;
-    default: x3::halo_launch<128, 64, 2, 2, 28, 2>(*p, splits, sk_grid, st); break;
+    case 6: x3::halo_launch<128, 64, 2, 2, 28, 2>(*p, splits, sk_grid, st); break;
+    case 7: x3::halo_launch<128, 64, 2, 2, x3::HALO_WMAX, 2>(*p, splits, sk_grid, st); break;
+    default: x3::halo_launch<64, 128, 2, 2, x3::HALO_WMAX, 2>(*p, splits, sk_grid, st); break;
   }
   return check_launch("conv_x3_halo_kernel");
 }
