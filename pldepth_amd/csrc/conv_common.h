@@ -51,6 +51,9 @@ struct GemmConvParams {
   int sk_nk, sk_tiles, sk_nnb, sk_align;
   float* sk_slab;
   int sk_q;  // steps per cut unit of a non-aligned range (0 / 1: any step)
+  // halo kernel grid order: 0 = N tiles fastest (the M tile's band shared in L2), 1 = M tiles
+  // fastest (the N panel of the filter shared in L2: filters larger than an XCD's L2)
+  int raster;
 };
 
 // first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)

@@ -411,8 +411,8 @@ __global__ __launch_bounds__(512, NB == 2 ? 2 : 1) void conv_x3_halo_kernel(Gemm
     kt_begin = (int)sk_begin(p, wid, nwg);
     kt_end = (int)sk_begin(p, wid + 1, nwg);
   } else {
-    nb = wid % nnb;  // (M tiles fastest instead measured no different)
-    mb = (wid / nnb) % nmb;
+    nb = p.raster ? (wid / nmb) % nnb : wid % nnb;
+    mb = p.raster ? wid % nmb : (wid / nnb) % nmb;
     zb = wid / (nnb * nmb);
     kt_begin = 0;
     kt_end = p.kc_tap * HALO_TAPS;
@@ -501,6 +501,13 @@ extern "C" int pld__x3_halo_launch(GemmConvParams* p, int cfg, int splits, int s
     return PLD_ERR_ARG;
   }
   hipStream_t st = as_stream(stream);
+  // grid order: M tiles fastest where the filter outgrows an XCD's 4 MB L2 (every N panel
+  // re-read per M tile otherwise); PLD_HALO_RASTER=0/1 forces one (A/B)
+  static const int raster_env = [] {
+    const char* e = std::getenv("PLD_HALO_RASTER");
+    return e ? std::atoi(e) : -1;
+  }();
+  p->raster = raster_env >= 0 ? raster_env : ((long)p->N * p->K * 4 > (4L << 20) ? 1 : 0);
   switch (cfg) {
     case 0: x3::halo_launch<256, 128, 2, 2, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
     case 1: x3::halo_launch<128, 256, 2, 2, x3::HALO_WMAX, 3>(*p, splits, sk_grid, st); break;
