@@ -324,13 +324,34 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   }
   setup(mb);
   lds_barrier();
-  if constexpr (!STREAM && NB == 3) {
+  // a tile's last step (or the range's): its sums out — whole tiles through the epilogue, a tile
+  // cut between workgroups as raw partials for the fixup kernel (STREAM)
+  auto tile_out = [&](int mbo, int nbo) {
+    const int first = tile * p.kc_tap;
+    if (first >= u0 && first + p.kc_tap <= u_end)
+      store_acc<TM, TN>(p, acc, mbo * BM + wm * WTM, nbo * BN + wn * WTN, lane);
+    else
+      store_partial<TM, TN, BM, BN>(p, acc, wm * WTM, wn * WTN, lane, wid,
+                                    tile == u0 / p.kc_tap ? 0 : 1);
+    zero();
+  };
+  if constexpr (NB == 3) {
     if (n > 0) read(0, 0, f0);
     for (int i = 0; i < n; ++i) {
       read(i, 1, f1);  // the second half of this step while the first multiplies
       mma(f0);
       interleave();
       __builtin_amdgcn_sched_barrier(0);
+      // STREAM: the last step of a tile; the next step (read below) is the next tile's first,
+      // so its rows and tap masks are set up now (this step's reads are all issued)
+      const bool tend = STREAM && i % HALO_TAPS == HALO_TAPS - 1 &&
+                        (kq == p.kc_tap - 1 || i == n - 1);
+      const int mbo = mb, nbo = nb;
+      if (STREAM && tend && i + 1 < n) {
+        mb = (tile + 1) / p.sk_nnb;
+        nb = tile + 1 - mb * p.sk_nnb;
+        setup(mb);
+      }
       // the next step's first half (ready since the last barrier: the producers run two steps
       // ahead); unconditional (the last step re-reads itself) so that the LDS wait counts stay
       // exact and this half's MFMAs do not wait for these reads
@@ -338,6 +359,17 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       mma(f1);
       interleave();
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (STREAM) {
+        if (i % HALO_TAPS == HALO_TAPS - 1) {
+          if (tend) {
+            tile_out(mbo, nbo);
+            ++tile;
+            kq = 0;
+          } else {
+            ++kq;
+          }
+        }
+      }
       // no LDS drain before this barrier: the reads still in flight are the next step's, from
       // buffers the producers do not write in the coming iteration (filter buffer (i + 1) % 3,
       // the current or next unit's patch); this step's reads completed under its MFMAs
@@ -345,8 +377,7 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       asm volatile("" ::: "memory");
     }
   } else {
-    // one step at a time (the tile stream: reading the next step ahead would need the next
-    // tile's rows across a tile boundary; NB == 2: the next filter slab is not there yet)
+    // NB == 2: one step at a time (the next step's filter slab is not there yet)
     for (int i = 0; i < n; ++i) {
       read(i, 0, f0);
       __builtin_amdgcn_sched_barrier(0);
@@ -354,17 +385,9 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
       read(i, 1, f0);
       __builtin_amdgcn_sched_barrier(0);
       mma(f0);
-      // a tile's last step (or the range's): its sums out — whole tiles through the epilogue, a
-      // tile cut between workgroups as raw partials for the fixup kernel
       if (STREAM && i % HALO_TAPS == HALO_TAPS - 1) {
         if (kq == p.kc_tap - 1 || i == n - 1) {
-          const int first = tile * p.kc_tap;
-          if (first >= u0 && first + p.kc_tap <= u_end)
-            store_acc<TM, TN>(p, acc, mb * BM + wm * WTM, nb * BN + wn * WTN, lane);
-          else
-            store_partial<TM, TN, BM, BN>(p, acc, wm * WTM, wn * WTN, lane, wid,
-                                          tile == u0 / p.kc_tap ? 0 : 1);
-          zero();
+          tile_out(mb, nb);
           ++tile;
           kq = 0;
           mb = tile / p.sk_nnb;
