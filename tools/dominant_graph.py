@@ -1,10 +1,11 @@
 """The dominant conv kernel's per-step time in graph replay, from a tools/kstats.py CSV of a
 rocprofv3 kernel trace of bench.py (the file bench.py --graph-profile reads).
 
-    python tools/dominant_graph.py KERNEL_STATS.csv STEPS OUT.json [--kernel conv_x3_kernel]
+    python tools/dominant_graph.py KERNEL_STATS.csv STEPS OUT.json [--kernel NAME | --bench BENCH.json]
 
 Sums every instantiation of the kernel (all tile / mode template arguments) over the window's
-STEPS steps; the workload string is bench.py's default cfg2 one."""
+STEPS steps; the workload string is bench.py's default cfg2 one. The kernel: --kernel, else the
+bench line's roofline.kernel (--bench), else conv_x3_kernel."""
 import argparse
 import csv
 import json
@@ -18,9 +19,14 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("steps", type=int)
     ap.add_argument("out")
-    ap.add_argument("--kernel", default="conv_x3_kernel")
+    ap.add_argument("--kernel", default="")
+    ap.add_argument("--bench", default="", help="bench.py JSON line: its dominant kernel")
     ap.add_argument("--source", default="")
     a = ap.parse_args()
+    if not a.kernel and a.bench:
+        with open(a.bench) as f:
+            a.kernel = json.loads(f.read().strip().splitlines()[-1])["roofline"]["kernel"]
+    a.kernel = a.kernel or "conv_x3_kernel"
     calls = ns = 0
     with open(a.csv) as f:
         for row in csv.DictReader(f):

@@ -34,7 +34,7 @@ python3 $R/tools/dominant_traffic.py $R/gpurun_out/pmc_step $O/bench.json $O/pmc
 cat $O/dom.log | tail -5
 WL="ff_effnet train step 448x448, per-GPU batch 32, ranking_size 5, rankings_per_image 100, sampler info, Adam-AMSGrad"
 python3 $R/tools/pmc_step_family.py $R/gpurun_out/pmc_step --workload "$WL" --json $O/pmc_step_family.json > $O/pmc_step_family.txt 2>&1
-python3 $R/tools/dominant_graph.py $O/kernel_stats.csv 10 $O/dominant_graph.json --source "profiles/${TAG}_kernel_stats.csv (rocprofv3 --kernel-trace of bench.py, 10 graph-replay steps, tools/kstats.py)" > /dev/null 2>&1
+python3 $R/tools/dominant_graph.py $O/kernel_stats.csv 10 $O/dominant_graph.json --bench $O/bench.json --source "profiles/${TAG}_kernel_stats.csv (rocprofv3 --kernel-trace of bench.py, 10 graph-replay steps, tools/kstats.py)" > /dev/null 2>&1
 rm -rf $O/trace
 bash $R/tools/prof_redweb.sh ${TAG}_rw > /dev/null 2>&1 || exit 1
 head -3 $R/gpurun_out/prof_${TAG}_rw/kstats.txt
