@@ -54,7 +54,19 @@ struct GemmConvParams {
   // halo kernel grid order: 0 = N tiles fastest (the M tile's band shared in L2), 1 = M tiles
   // fastest (the N panel of the filter shared in L2: filters larger than an XCD's L2)
   int raster;
+  // tile-stream tile order (halo kernel): sk_perm = P > 1 maps stream tile t to tile
+  // (t % P) Q + t / P over the first P Q tiles (Q = sk_tiles / P); 0 / 1: identity (sk_tile)
+  int sk_perm;
 };
+
+// the tile at stream position t. With workgroup ranges about P tiles long, P-way interleaving
+// puts consecutive workgroups — one XCD's, which run together — on neighbouring tiles (whose
+// input bands overlap in that XCD's L2) instead of P tiles apart
+__host__ __device__ inline int sk_tile(const GemmConvParams& p, int t) {
+  if (p.sk_perm <= 1) return t;
+  const int q = p.sk_tiles / p.sk_perm;
+  return t < q * p.sk_perm ? (t % p.sk_perm) * q + t / p.sk_perm : t;
+}
 
 // first global step of workgroup w of G in the tile-stream schedule (GemmConvParams sk_*)
 // XCD-aware workgroup order: workgroups are dealt round-robin to the 8 XCDs (flat ids b, b + 8,

@@ -643,7 +643,8 @@ __global__ __launch_bounds__(256) void x3_stream_fixup_kernel(GemmConvParams p, 
   if (sk_begin(p, j - 1, G) > ts) return;  // an earlier cut of the same tile handles it
   const long c0 = sk_owner(p, ts, G), c1 = sk_owner(p, ts + nk - 1, G);
   const int col = threadIdx.x;
-  const int mb = (int)(t / p.sk_nnb), nb = (int)(t - (long)mb * p.sk_nnb);
+  const int ta = sk_tile(p, (int)t);
+  const int mb = ta / p.sk_nnb, nb = ta - mb * p.sk_nnb;
   const int gc = nb * BN + col;
   if (col >= BN || gc >= p.N) return;
   const float bias = p.bias ? p.bias[gc] : 0.f;

@@ -87,8 +87,9 @@ __device__ __forceinline__ void halo_producer(const GemmConvParams& p, unsigned 
     if constexpr (STREAM) {
       const int u = u0 + gc, t = u / p.kc_tap;
       c.kq = u - t * p.kc_tap;
-      mb = t / p.sk_nnb;
-      nb = t - mb * p.sk_nnb;
+      const int ta = sk_tile(p, t);
+      mb = ta / p.sk_nnb;
+      nb = ta - mb * p.sk_nnb;
     } else {
       c.kq = u0 + gc;
     }
@@ -319,8 +320,8 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
   if constexpr (STREAM) {
     tile = u0 / p.kc_tap;
     kq = u0 - tile * p.kc_tap;
-    mb = tile / p.sk_nnb;
-    nb = tile - mb * p.sk_nnb;
+    mb = sk_tile(p, tile) / p.sk_nnb;
+    nb = sk_tile(p, tile) - mb * p.sk_nnb;
   }
   setup(mb);
   lds_barrier();
@@ -348,8 +349,9 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
                         (kq == p.kc_tap - 1 || i == n - 1);
       const int mbo = mb, nbo = nb;
       if (STREAM && tend && i + 1 < n) {
-        mb = (tile + 1) / p.sk_nnb;
-        nb = tile + 1 - mb * p.sk_nnb;
+        const int ta = sk_tile(p, tile + 1);
+        mb = ta / p.sk_nnb;
+        nb = ta - mb * p.sk_nnb;
         setup(mb);
       }
       // the next step's first half (ready since the last barrier: the producers run two steps
@@ -390,8 +392,8 @@ __device__ __forceinline__ void halo_consumer(const GemmConvParams& p, unsigned 
           tile_out(mb, nb);
           ++tile;
           kq = 0;
-          mb = tile / p.sk_nnb;
-          nb = tile - mb * p.sk_nnb;
+          mb = sk_tile(p, tile) / p.sk_nnb;
+          nb = sk_tile(p, tile) - mb * p.sk_nnb;
           setup(mb);
         } else {
           ++kq;
@@ -559,6 +561,13 @@ extern "C" int pld__x3_halo_stream_plan(GemmConvParams* p, int cfg) {
   const long G = std::max<long>(1, std::min<long>(256L * (x3::kHalo[cfg].nb == 2 ? 2 : 1),
                                                   units / 4));
   p->sk_align = (tiles % G == 0) ? 1 : 0;
+  // P-way interleaved tile order where each workgroup walks P >= 2 tiles (sk_tile);
+  // PLD_HALO_PERM=0 keeps the plain order (A/B)
+  static const int perm_env = [] {
+    const char* e = std::getenv("PLD_HALO_PERM");
+    return e ? std::atoi(e) : 1;
+  }();
+  p->sk_perm = perm_env && tiles >= 2 * G ? (int)((tiles + G / 2) / G) : 0;
   return (int)G;
 }
 extern "C" size_t pld__x3_halo_stream_slab_bytes(int cfg, int G, int aligned) {

@@ -278,7 +278,11 @@ def test_conv_every_schedule(cuda, case, math):
     # dec2-like: the widest map the kernel takes (56), patch rows = BM + 114
     (1, 56, 56, 96, 0, 144, True),
     # a band straddling images on a map narrower than a tile row, odd width and height
-    (3, 9, 13, 40, 24, 72, True)])
+    (3, 9, 13, 40, 24, 72, True),
+    # tile streams with >= 2 tiles per workgroup: the interleaved tile order (sk_perm 2 and 4,
+    # a non-permuted tail tile)
+    (2, 28, 28, 48, 0, 64, False),
+    (4, 56, 56, 32, 0, 40, True)])
 def test_conv_halo_schedules(cuda, case):
     """The row-band halo kernel (every x3halo / x3halosplit schedule): fwd with bias and
     accumulate, dgrad into a concat's two destinations (one accumulating), against fp64; the
