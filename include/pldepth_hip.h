@@ -389,7 +389,8 @@ int pld_upconv_wgrad(const float* x, int n, int h, int w, int c, const float* me
 int pld_upconv_dgrad(const float* dy, int n, int h, int w, int c, const float* wt, float* dact,
                      void* stream);
 /* y = a * sample_scale[img] + b  (EfficientNet drop-connect Dropout(noise_shape=(N,1,1,1)) +
- * residual add); sample_scale may be NULL (=1). rows_per_img*c elements per image. */
+ * residual add; the product and the sum rounded separately, as Keras' two layers);
+ * sample_scale may be NULL (=1). rows_per_img*c elements per image. */
 int pld_residual_add(const float* a, const float* sample_scale, const float* b, int n,
                      int64_t elems_per_img, float* y, void* stream);
 /* Dropout(rate, noise_shape=(N,1,1,1)) keep factors for drop-connect: scales[i] = keep ? 1/(1-rate)

@@ -377,13 +377,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
 #pragma unroll
       for (int u = 0; u < VW; ++u) xv[u] = xv[u] * mu[u] + is[u];
     }
-    if (p.sscale) {  // drop-connect scale of the BN output: fma with the residual, as residual_add
+    if (p.sscale) {  // drop-connect scale of the BN output, then + the residual: two roundings, as
+                     // Keras' Dropout product and Add (and residual_add)
       const float sc = p.sscale[p.dHW.div((uint32_t)p.dCV.div((uint32_t)e))];
       if (p.res) {
         float rv[VW];
         ld<VW>(p.res + e * VW, rv);
 #pragma unroll
-        for (int u = 0; u < VW; ++u) xv[u] = fmaf(xv[u], sc, rv[u]);
+        for (int u = 0; u < VW; ++u) xv[u] = __fadd_rn(__fmul_rn(xv[u], sc), rv[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < VW; ++u) xv[u] = __fmul_rn(xv[u], sc);

@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long)gridDim.x * blockDim.x) {
     const float s = sc ? sc[e / per] : 1.f;
-    float v = b ? fmaf(a[e], s, b[e]) : __fmul_rn(a[e], s);  // one rounding, as bn_scale_add_apply
+    // the product and the sum rounded separately (Keras Dropout, then Add)
+    float v = b ? __fadd_rn(__fmul_rn(a[e], s), b[e]) : __fmul_rn(a[e], s);
     if (acc) v = __fadd_rn(v, y[e]);
     y[e] = v;
   }
@@ -286,9 +287,10 @@ __global__ __launch_bounds__(256) void residual4_kernel(const float4* __restrict
     const float s = sc ? sc[dPer4.div(e)] : 1.f;
     const float4 u = a[e];
     float4 v;
-    if (b) {  // fma: one rounding, as pld_bn_scale_add_apply
+    if (b) {  // product and sum rounded separately, as residual_kernel
       const float4 w = b[e];
-      v = make_float4(fmaf(u.x, s, w.x), fmaf(u.y, s, w.y), fmaf(u.z, s, w.z), fmaf(u.w, s, w.w));
+      v = make_float4(__fadd_rn(__fmul_rn(u.x, s), w.x), __fadd_rn(__fmul_rn(u.y, s), w.y),
+                      __fadd_rn(__fmul_rn(u.z, s), w.z), __fadd_rn(__fmul_rn(u.w, s), w.w));
     } else {
       v = make_float4(__fmul_rn(u.x, s), __fmul_rn(u.y, s), __fmul_rn(u.z, s), __fmul_rn(u.w, s));
     }

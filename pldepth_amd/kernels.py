@@ -812,12 +812,21 @@ def dropconnect_scales_multi(scales, rates, layers, seed, step, image_offset=0):
     import ctypes
     nl = len(layers)
     assert scales.dim() == 2 and scales.shape[0] == nl and scales.is_contiguous()
-    r = (ctypes.c_float * nl)(*[float(x) for x in rates])
-    l = (ctypes.c_int * nl)(*[int(x) for x in layers])
+    assert len(rates) == nl
     dev = isinstance(step, torch.Tensor)
-    lib().pld_dropconnect_scales_multi(ptr(scales), scales.shape[1], nl, ctypes.cast(r, ctypes.c_void_p),
-                                       ctypes.cast(l, ctypes.c_void_p), seed, 0 if dev else step,
-                                       ptr(step) if dev else None, image_offset, stream())
+    # one launch per DC_MAX_LAYERS rows (the kernel's parameter block; EfficientNetB0 has 16)
+    for s0 in range(0, nl, DC_MAX_LAYERS):
+        m = min(DC_MAX_LAYERS, nl - s0)
+        r = (ctypes.c_float * m)(*[float(x) for x in rates[s0:s0 + m]])
+        l = (ctypes.c_int * m)(*[int(x) for x in layers[s0:s0 + m]])
+        lib().pld_dropconnect_scales_multi(ptr(scales[s0:s0 + m]), scales.shape[1], m,
+                                           ctypes.cast(r, ctypes.c_void_p),
+                                           ctypes.cast(l, ctypes.c_void_p), seed,
+                                           0 if dev else step, ptr(step) if dev else None,
+                                           image_offset, stream())
+
+
+DC_MAX_LAYERS = 32  # pld_dropconnect_scales_multi rows per launch (resample.hip)
 
 
 def bn_train_coeffs(mean, invstd, gamma, beta, scale, shift):

@@ -165,12 +165,16 @@ class _Conv:
 
 def refresh_trainable_convs(eng):
     """Every trainable conv's filter copies after the optimizer step, in one launch
-    (kernels.FilterRefreshBatch over a descriptor table built at the first call: the engines
-    make it eagerly, from set_weights, before any graph capture)."""
+    (kernels.FilterRefreshBatch over a device descriptor table of raw pointers). The table is
+    built at the first call — an eager step always precedes a graph capture — and rebuilt when
+    any conv's buffers were rebound since (the pointers it holds are compared with the convs'
+    current tensors on every eager call), so it never writes through stale pointers; a capture
+    that would need a rebuild fails instead."""
+    entries = [(c.w, c.w_nat, c.w_nat_x3, c.w_dg, c.w_dg_x3) for c in eng.convs if c.trainable]
+    key = [tuple(None if t is None else t.data_ptr() for t in e) for e in entries]
     batch = getattr(eng, "_refresh_batch", None)
-    if batch is None:
-        assert not K._CAPTURING[0], "the refresh table must be built before graph capture"
-        batch = eng._refresh_batch = K.FilterRefreshBatch(
-            [(c.w, c.w_nat, c.w_nat_x3, c.w_dg, c.w_dg_x3) for c in eng.convs if c.trainable],
-            eng.device)
+    if batch is None or getattr(eng, "_refresh_key", None) != key:
+        assert not K._CAPTURING[0], "the refresh table must be (re)built before graph capture"
+        batch = eng._refresh_batch = K.FilterRefreshBatch(entries, eng.device)
+        eng._refresh_key = key
     batch()

@@ -397,6 +397,20 @@ def test_dropconnect_scales_multi_layer_launch(cuda):
                     got[s], PX.dropconnect_scales(n, r, seed, step, layer=li, image_offset=6))
 
 
+def test_dropconnect_scales_multi_more_layers_than_one_launch(cuda):
+    """More blocks than one launch's parameter block (kernels.DC_MAX_LAYERS): split into
+    launches, every row still its own layer's stream."""
+    n, seed, step = 11, 9, 4
+    nl = K.DC_MAX_LAYERS + 5
+    rates = [0.01 * (1 + i % 20) for i in range(nl)]
+    layers = list(range(2, 2 + nl))
+    out = torch.full((nl, n), -1.0, device=cuda)
+    K.dropconnect_scales_multi(out, rates, layers, seed, step)
+    got = out.cpu().numpy()
+    for s, (r, li) in enumerate(zip(rates, layers)):
+        np.testing.assert_array_equal(got[s], PX.dropconnect_scales(n, r, seed, step, layer=li))
+
+
 def test_sampler_draws_bit_exact_vs_philox(cuda):
     nv = np.array([1, 7, 1000, 200704], np.int32)
     d = torch.empty(4, 500, 5, dtype=torch.int32, device=cuda)

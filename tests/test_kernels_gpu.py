@@ -666,7 +666,8 @@ def test_residual_and_per_sample_scale(cuda):
     sc = torch.tensor([0.0, 1.25, 1.25])
     y = torch.empty(3, 4, 5, 8, device=cuda)
     K.residual_add(a.to(cuda), sc.to(cuda), b.to(cuda), y)
-    torch.testing.assert_close(y.cpu(), a * sc.view(3, 1, 1, 1) + b)
+    # bit for bit the two-step fp32 form (Keras: Dropout's product rounded, then Add's sum)
+    torch.testing.assert_close(y.cpu(), a * sc.view(3, 1, 1, 1) + b, rtol=0, atol=0)
     K.scale_per_sample(a.to(cuda), sc.to(cuda), y, accumulate=True)
     torch.testing.assert_close(y.cpu(), 2 * a * sc.view(3, 1, 1, 1) + b)
 
@@ -680,7 +681,7 @@ def test_residual_inplace_vector_and_scalar_paths(cuda, shape):
     sc = torch.rand(shape[0]) + 0.5
     ga = a.to(cuda)
     K.residual_add(ga, sc.to(cuda), b.to(cuda), ga)
-    torch.testing.assert_close(ga.cpu(), a * sc.view(-1, 1, 1, 1) + b)
+    torch.testing.assert_close(ga.cpu(), a * sc.view(-1, 1, 1, 1) + b, rtol=0, atol=0)
     gb = a.to(cuda)
     K.residual_add(gb, None, b.to(cuda), gb)
     torch.testing.assert_close(gb.cpu(), a + b)
@@ -1107,6 +1108,12 @@ def test_bn_scale_add_fused_matches_unfused(cuda, n, hw, c):
     K.bn_bwd_scaled(x, dy, rows, c, gm, gi, gam, bet, "none", sc, hw, dx, dg, db)
     torch.cuda.synchronize()
     assert torch.equal(y, y_un)
+    # ... and to the reference's two-step fp32 form: Dropout's product rounded, then Add's sum
+    y_bn = torch.empty_like(x)
+    K.bn_apply(x, rows, c, gm, gi, gam, bet, "none", y_bn)
+    two_step = y_bn.view(n, hw, c) * sc.view(n, 1, 1) + res.view(n, hw, c)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(n, hw, c), two_step)
     assert torch.equal(dx, dx_un)
     assert torch.equal(dg, dg_un) and torch.equal(db, db_un)
     # a dropped image passes only its residual
