@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
           if (p.sscale) {  // drop-connect: d(bn out) = dy * scale[img], rounded as its own product
             const float sc = p.sscale[p.dHW.div((uint32_t)(r + j * rpi))];
 #pragma unroll
-            for (int u = 0; u < VW; ++u) dv[j][u] = __fmul_rn(dv[j][u], sc);
+            for (int u = 0; u < VW; ++u) dv[j][u] = mul_rn(dv[j][u], sc);
           }
           if (p.res) {
             ld<VW>(p.res + (r + j * rpi) * p.C + c0, rv[j]);
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(RedParams p) {
         if (p.sscale) {
           const float sc = p.sscale[img];
 #pragma unroll
-          for (int u = 0; u < VW; ++u) dv[u] = __fmul_rn(dv[u], sc);
+          for (int u = 0; u < VW; ++u) dv[u] = mul_rn(dv[u], sc);
         }
 #pragma unroll
         for (int u = 0; u < VW; ++u) { g[u] = 1.f; a[u] = 0.f; }
@@ -384,16 +384,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(ApplyParams p) {
         float rv[VW];
         ld<VW>(p.res + e * VW, rv);
 #pragma unroll
-        for (int u = 0; u < VW; ++u) xv[u] = __fadd_rn(__fmul_rn(xv[u], sc), rv[u]);
+        for (int u = 0; u < VW; ++u) xv[u] = add_rn(mul_rn(xv[u], sc), rv[u]);
       } else {
 #pragma unroll
-        for (int u = 0; u < VW; ++u) xv[u] = __fmul_rn(xv[u], sc);
+        for (int u = 0; u < VW; ++u) xv[u] = mul_rn(xv[u], sc);
       }
     } else if (p.res) {
       float rv[VW];
       ld<VW>(p.res + e * VW, rv);
 #pragma unroll
-      for (int u = 0; u < VW; ++u) xv[u] = __fadd_rn(xv[u], rv[u]);
+      for (int u = 0; u < VW; ++u) xv[u] = add_rn(xv[u], rv[u]);
     }
 #pragma unroll
     for (int u = 0; u < VW; ++u) g[u] = 1.f;
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BwdApplyParams p) {
       if (p.sscale) {
         const float sc = p.sscale[img];
 #pragma unroll
-        for (int u = 0; u < VW; ++u) dv[u] = __fmul_rn(dv[u], sc);
+        for (int u = 0; u < VW; ++u) dv[u] = mul_rn(dv[u], sc);
       }
     }
     float rv[VW];

@@ -34,6 +34,20 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ---- fp32 operations rounded on their own ----
+// HIP's __fmul_rn / __fadd_rn are the plain operators (clang's HIP math header), which hipcc's
+// default -ffp-contract=fast-honor-pragmas may fuse into one fma with a neighbouring add. These
+// never fuse: for arithmetic that must round like the reference's separate NumPy / Keras ops
+// (a drop-connect product then the residual sum; np.linspace's arange * step + start).
+__device__ __forceinline__ float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
 // ---- activations (Keras semantics) ----
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
 

@@ -269,8 +269,8 @@ __global__ __launch_bounds__(256) void residual_kernel(const float* __restrict__
        e += (long)gridDim.x * blockDim.x) {
     const float s = sc ? sc[e / per] : 1.f;
     // the product and the sum rounded separately (Keras Dropout, then Add)
-    float v = b ? __fadd_rn(__fmul_rn(a[e], s), b[e]) : __fmul_rn(a[e], s);
-    if (acc) v = __fadd_rn(v, y[e]);
+    float v = b ? add_rn(mul_rn(a[e], s), b[e]) : mul_rn(a[e], s);
+    if (acc) v = add_rn(v, y[e]);
     y[e] = v;
   }
 }
@@ -289,10 +289,10 @@ __global__ __launch_bounds__(256) void residual4_kernel(const float4* __restrict
     float4 v;
     if (b) {  // product and sum rounded separately, as residual_kernel
       const float4 w = b[e];
-      v = make_float4(__fadd_rn(__fmul_rn(u.x, s), w.x), __fadd_rn(__fmul_rn(u.y, s), w.y),
-                      __fadd_rn(__fmul_rn(u.z, s), w.z), __fadd_rn(__fmul_rn(u.w, s), w.w));
+      v = make_float4(add_rn(mul_rn(u.x, s), w.x), add_rn(mul_rn(u.y, s), w.y),
+                      add_rn(mul_rn(u.z, s), w.z), add_rn(mul_rn(u.w, s), w.w));
     } else {
-      v = make_float4(__fmul_rn(u.x, s), __fmul_rn(u.y, s), __fmul_rn(u.z, s), __fmul_rn(u.w, s));
+      v = make_float4(mul_rn(u.x, s), mul_rn(u.y, s), mul_rn(u.z, s), mul_rn(u.w, s));
     }
     y[e] = v;
   }

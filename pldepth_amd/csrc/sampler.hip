@@ -162,7 +162,7 @@ __global__ void draw_kernel(const int* __restrict__ nvalid, int B, int per_img, 
 __device__ __forceinline__ int depth_relation32(float d1, float d2) {
   // pldepth/data/depth_utils.py:5-21 with tau = 0.03, float32 (NumPy 2 / NEP 50)
   const float eps = 1e-10f;
-  const float r = __fdiv_rn(__fadd_rn(d1, eps), __fadd_rn(d2, eps));
+  const float r = __fdiv_rn(add_rn(d1, eps), add_rn(d2, eps));
   if (r >= 1.03f) return 1;
   if (r <= (float)(1.0 / 1.03)) return -1;  // float32(1/1.03), as NumPy casts the Python float
   return 0;
@@ -173,7 +173,7 @@ __device__ float pairwise_sum32(const float* a, int n) {
   // iterative form of the recursion: the recursion only splits when n > 128
   if (n < 8) {
     float res = -0.0f;
-    for (int i = 0; i < n; ++i) res = __fadd_rn(res, a[i]);
+    for (int i = 0; i < n; ++i) res = add_rn(res, a[i]);
     return res;
   }
   if (n <= 128) {
@@ -181,19 +181,19 @@ __device__ float pairwise_sum32(const float* a, int n) {
     for (int j = 0; j < 8; ++j) r[j] = a[j];
     int i = 8;
     for (; i < n - (n % 8); i += 8)
-      for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], a[i + j]);
-    float res = __fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3]));
-    res = __fadd_rn(res, __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
-    for (; i < n; ++i) res = __fadd_rn(res, a[i]);
+      for (int j = 0; j < 8; ++j) r[j] = add_rn(r[j], a[i + j]);
+    float res = add_rn(add_rn(r[0], r[1]), add_rn(r[2], r[3]));
+    res = add_rn(res, add_rn(add_rn(r[4], r[5]), add_rn(r[6], r[7])));
+    for (; i < n; ++i) res = add_rn(res, a[i]);
     return res;
   }
   int n2 = n / 2;
   n2 -= n2 % 8;
-  return __fadd_rn(pairwise_sum32(a, n2), pairwise_sum32(a + n2, n - n2));
+  return add_rn(pairwise_sum32(a, n2), pairwise_sum32(a + n2, n - n2));
 }
 
 __device__ float pairwise_sum32_top(const float* a, int n) {
-  return __fadd_rn(0.0f, pairwise_sum32(a, n));
+  return add_rn(0.0f, pairwise_sum32(a, n));
 }
 
 struct RankParams {
@@ -262,21 +262,21 @@ __global__ __launch_bounds__(256) void candidate_kernel(RankParams p) {
       float acc = 0.0f;
       for (int j = 0; j + 1 < L; ++j) {
         if (p.strategy == PLD_SAMPLER_THRESH && depth_relation32(g[j], g[j + 1]) == 0)
-          acc = __fadd_rn(acc, -1000.0f);
-        acc = __fadd_rn(acc, fabsf(__fsub_rn(g[j], g[j + 1])));
+          acc = add_rn(acc, -1000.0f);
+        acc = add_rn(acc, fabsf(__fsub_rn(g[j], g[j + 1])));
       }
       sc = (double)acc;
     } else if (p.strategy == PLD_SAMPLER_INFO) {
       // expected = np.linspace(min+0.001, max, L+1)[1:] in float32
-      const float start = __fadd_rn(p.gt_minmax[2 * b], 0.001f);
+      const float start = add_rn(p.gt_minmax[2 * b], 0.001f);
       const float stop = p.gt_minmax[2 * b + 1];
       const float delta = __fsub_rn(stop, start);
       const float stepv = __fdiv_rn(delta, (float)L);
       float t[LMAX];
       for (int j = 0; j < L; ++j) {
-        const float ev = (j == L - 1) ? stop : __fadd_rn(__fmul_rn((float)(j + 1), stepv), start);
+        const float ev = (j == L - 1) ? stop : add_rn(mul_rn((float)(j + 1), stepv), start);
         const float d = __fsub_rn(g[j], ev);
-        t[j] = __fdiv_rn(__fmul_rn(d, d), ev);
+        t[j] = __fdiv_rn(mul_rn(d, d), ev);
       }
       sc = -(double)pairwise_sum32_top(t, L);
       for (int j = 0; j + 1 < L; ++j)
@@ -328,19 +328,19 @@ __global__ __launch_bounds__(256) void candidate_wave_kernel(RankParams p) {
       for (int j = 0; j + 1 < L; ++j) {
         const float gj1 = __shfl(gs, j + 1, 64);
         if (p.strategy == PLD_SAMPLER_THRESH && depth_relation32(gj, gj1) == 0)
-          acc = __fadd_rn(acc, -1000.0f);
-        acc = __fadd_rn(acc, fabsf(__fsub_rn(gj, gj1)));
+          acc = add_rn(acc, -1000.0f);
+        acc = add_rn(acc, fabsf(__fsub_rn(gj, gj1)));
         gj = gj1;
       }
       sc = (double)acc;
     } else if (p.strategy == PLD_SAMPLER_INFO) {
-      const float start = __fadd_rn(p.gt_minmax[2 * b], 0.001f);
+      const float start = add_rn(p.gt_minmax[2 * b], 0.001f);
       const float stop = p.gt_minmax[2 * b + 1];
       const float stepv = __fdiv_rn(__fsub_rn(stop, start), (float)L);
       const float ev =
-          (lane == L - 1) ? stop : __fadd_rn(__fmul_rn((float)(lane + 1), stepv), start);
+          (lane == L - 1) ? stop : add_rn(mul_rn((float)(lane + 1), stepv), start);
       const float dd = __fsub_rn(gs, ev);
-      const float t = __fdiv_rn(__fmul_rn(dd, dd), ev);
+      const float t = __fdiv_rn(mul_rn(dd, dd), ev);
       // pairwise_sum32, 8 <= n <= 128 branch
       float r[8];
 #pragma unroll
@@ -349,11 +349,11 @@ __global__ __launch_bounds__(256) void candidate_wave_kernel(RankParams p) {
       int i = 8;
       for (; i < nfull; i += 8)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], __shfl(t, i + j, 64));
-      float res = __fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3]));
-      res = __fadd_rn(res, __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
-      for (; i < L; ++i) res = __fadd_rn(res, __shfl(t, i, 64));
-      sc = -(double)__fadd_rn(0.0f, res);
+        for (int j = 0; j < 8; ++j) r[j] = add_rn(r[j], __shfl(t, i + j, 64));
+      float res = add_rn(add_rn(r[0], r[1]), add_rn(r[2], r[3]));
+      res = add_rn(res, add_rn(add_rn(r[4], r[5]), add_rn(r[6], r[7])));
+      for (; i < L; ++i) res = add_rn(res, __shfl(t, i, 64));
+      sc = -(double)add_rn(0.0f, res);
       const float gn = __shfl(gs, min(lane + 1, 63), 64);
       const int nz = __popcll(__ballot(lane + 1 < L && depth_relation32(gs, gn) == 0));
       for (int k = 0; k < nz; ++k) sc = __dadd_rn(sc, -1000.0);
