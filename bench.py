@@ -675,14 +675,14 @@ def main():
                     help="conv arithmetic policy (kernels.conv_policy): auto = decoder bf16x3, "
                          "encoder bf16x3 where the BN sees >= 4096 values per channel (all of "
                          "them at 448x448 batch 32); mixed = encoder fp32, decoder bf16x3")
-    ap.add_argument("--traffic-profile", default="profiles/r06b_pmc_dominant.json",
+    ap.add_argument("--traffic-profile", default="profiles/r06c_pmc_dominant.json",
                     help="PMC traffic of the dominant kernel (tools/dominant_traffic.py, committed "
                          "from the same HEAD and workload): fills roofline.traffic when its kernel "
                          "and workload match this run's")
-    ap.add_argument("--graph-profile", default="profiles/r06b_dominant_graph.json",
+    ap.add_argument("--graph-profile", default="profiles/r06c_dominant_graph.json",
                     help="rocprof time of the dominant kernel inside the whole-step graph replays "
                          "(roofline.rocprof_step_replay)")
-    ap.add_argument("--step-traffic-profile", default="profiles/r06b_pmc_step_family.json",
+    ap.add_argument("--step-traffic-profile", default="profiles/r06c_pmc_step_family.json",
                     help="PMC HBM bytes of one eager step per op family "
                          "(tools/pmc_step_family.py): roofline.step_bytes_measured")
     ap.add_argument("--schedules", default="",
